@@ -1,0 +1,204 @@
+/* SPDX-License-Identifier: GPL-2.0 */
+/*
+ * xdpfilter_gpu.h — C ABI of the MI355X-native xdp-filter classifier.
+ *
+ * This is the drop-in boundary for xdp-filter's per-packet hot path: the ten
+ * eBPF programs xdpfilt_{alw,dny}_{all,eth,ip,tcp,udp} built from
+ * xdp-filter/xdpfilt_prog.h:214-310 (reference v1.6.3), their BPF maps
+ * (xdp-filter/xdpfilt_prog.h:67-185, headers/xdp/xdp_stats_kern.h:20-26) and
+ * the userspace operations the xdp-filter CLI performs on them
+ * (xdp-filter/xdp-filter.c:48-157).  The per-packet program becomes a batch
+ * HIP kernel over packets resident in HBM; the per-CPU BPF maps become
+ * per-device tables whose values keep the reference encoding
+ * (hits << COUNTER_SHIFT) | flags.
+ *
+ * Plain C types only (no HIP/torch types): streams are passed as void*
+ * (a hipStream_t, or NULL for the device's default stream of this library).
+ * Errors are negative errno values, as in libxdp/libbpf
+ * (headers/xdp/libxdp.h:51-53).
+ */
+#ifndef XDPFILTER_GPU_H
+#define XDPFILTER_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants: identical values to xdp-filter/common_kern_user.h:4-19 ---- */
+#define XFG_FEAT_TCP      (1u << 0)
+#define XFG_FEAT_UDP      (1u << 1)
+#define XFG_FEAT_IPV6     (1u << 2)
+#define XFG_FEAT_IPV4     (1u << 3)
+#define XFG_FEAT_ETHERNET (1u << 4)
+#define XFG_FEAT_ALL      (XFG_FEAT_TCP | XFG_FEAT_UDP | XFG_FEAT_IPV6 | \
+			   XFG_FEAT_IPV4 | XFG_FEAT_ETHERNET)
+#define XFG_FEAT_ALLOW    (1u << 5)
+#define XFG_FEAT_DENY     (1u << 6)
+
+#define XFG_MAP_FLAG_SRC  (1u << 0)
+#define XFG_MAP_FLAG_DST  (1u << 1)
+#define XFG_MAP_FLAG_TCP  (1u << 2)
+#define XFG_MAP_FLAG_UDP  (1u << 3)
+#define XFG_MAP_FLAGS     (XFG_MAP_FLAG_SRC | XFG_MAP_FLAG_DST | \
+			   XFG_MAP_FLAG_TCP | XFG_MAP_FLAG_UDP)
+#define XFG_COUNTER_SHIFT 6
+
+/* enum xdp_action values (headers/linux/bpf.h:6130-6136) */
+#define XFG_XDP_ABORTED   0
+#define XFG_XDP_DROP      1
+#define XFG_XDP_PASS      2
+#define XFG_ACTION_MAX    5   /* XDP_REDIRECT + 1, headers/xdp/xdp_stats_kern_user.h:21 */
+
+/* Default hash-map capacity = the reference's max_entries
+ * (xdp-filter/xdpfilt_prog.h:115,146,181). */
+#define XFG_DEFAULT_MAP_CAPACITY 10000u
+#define XFG_PORT_MAP_ENTRIES     65536u   /* xdp-filter/xdpfilt_prog.h:69 */
+
+/* Maps, named as the reference pins them (xdp-filter/common_kern_user.h:21-24). */
+enum xfg_map_id {
+	XFG_MAP_PORTS    = 0, /* "filter_ports":    key u32 = raw be16 port (htons(port)), PERCPU_ARRAY */
+	XFG_MAP_IPV4     = 1, /* "filter_ipv4":     key 4 bytes, network order */
+	XFG_MAP_IPV6     = 2, /* "filter_ipv6":     key 16 bytes (struct in6_addr) */
+	XFG_MAP_ETHERNET = 3, /* "filter_ethernet": key 6 bytes (struct ethaddr) */
+	XFG_MAP_NUM      = 4,
+};
+
+/* struct xdp_stats_record, headers/xdp/xdp_stats_kern_user.h:10-19 */
+struct xfg_stats_record {
+	uint64_t packets;
+	uint64_t bytes;
+};
+
+typedef struct xfg_ctx xfg_ctx;
+
+struct xfg_open_opts {
+	size_t sz;               /* sizeof(struct xfg_open_opts), for extension */
+	uint32_t features;       /* XFG_FEAT_* requested | XFG_FEAT_ALLOW or _DENY */
+	const int *devices;      /* HIP device ordinals; NULL with ndev>0 => 0..ndev-1 */
+	int ndev;                /* 0 => host-only context: map CRUD works, classify -ENODEV */
+	uint32_t ipv4_capacity;  /* 0 => XFG_DEFAULT_MAP_CAPACITY */
+	uint32_t ipv6_capacity;
+	uint32_t eth_capacity;
+	uint32_t hash_seed;      /* 0 => fixed default seed */
+};
+
+/*
+ * Program selection, same rule as find_prog_file() (xdp-filter/xdp-filter.c:48-60):
+ * the first program in xdp-filter/Makefile:3-6 order whose feature bits are a
+ * superset of @features.  Returns 0 and the program's name/features, or
+ * -ENOENT (no program matches, e.g. ALLOW|DENY both set) / -EINVAL (0).
+ */
+int xfg_select_program(uint32_t features, const char **prog_name,
+		       uint32_t *prog_features);
+
+/* Open a context: selects the program, allocates the tables on every device. */
+int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts);
+void xfg_close(xfg_ctx *ctx);
+
+const char *xfg_prog_name(const xfg_ctx *ctx);      /* e.g. "xdpfilt_dny_all" */
+uint32_t xfg_prog_features(const xfg_ctx *ctx);     /* the program's _features word */
+int xfg_num_devices(const xfg_ctx *ctx);            /* analogue of libbpf_num_possible_cpus() */
+const char *xfg_strerror(int err);
+
+/*
+ * Map operations.  As with a BPF per-CPU map, a value is one u64 per device
+ * (vals[xfg_num_devices()]), or exactly one u64 on a host-only context.
+ *   lookup:  -ENOENT if the key is absent (hash maps); ports always exist.
+ *   update:  insert or overwrite; -E2BIG when a hash map is full.
+ *   delete:  -ENOENT if absent; ports: -EINVAL (array maps cannot delete).
+ *   get_next_key: key==NULL => first key; -ENOENT after the last one.
+ * Key sizes: ports 4 (u32, < 65536), ipv4 4, ipv6 16, ethernet 6.
+ */
+int xfg_map_lookup(xfg_ctx *ctx, int map, const void *key, uint64_t *vals);
+int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals);
+int xfg_map_delete(xfg_ctx *ctx, int map, const void *key);
+int xfg_map_get_next_key(xfg_ctx *ctx, int map, const void *key, void *next_key);
+/* Number of keys present (ports: number of non-zero entries). */
+int64_t xfg_map_count(xfg_ctx *ctx, int map);
+/* Bulk insert/overwrite of @n keys with the same value on every device
+ * (rule-set loading).  Returns 0 or the first error (-E2BIG, ...). */
+int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t *vals,
+			 uint64_t n);
+
+/*
+ * A packet batch resident on ONE device.  Packet i starts at
+ *   data + (offsets ? offsets[i] : i * stride)
+ * and is lens[i] bytes long (u16 lens if lens_u16, else u32).  Every packet
+ * start must be 16-byte aligned and the buffer readable up to the next
+ * 16-byte boundary past its end (AF_XDP UMEM chunks and the pcap/synthetic
+ * ingest paths of this library satisfy this).  Packet length is not limited
+ * by stride when offsets are given.
+ */
+struct xfg_batch {
+	const void *data;
+	const uint64_t *offsets;
+	const void *lens;
+	uint64_t count;
+	uint32_t stride;
+	uint32_t lens_u16;
+};
+
+/*
+ * Classify a device-resident batch on device @dev (index into the context's
+ * devices): writes one enum xdp_action byte per packet to @verdicts (device
+ * memory), bumps the matched rule's counter on that device and records
+ * per-action stats, exactly as xdpfilt_<mode>() + xdp_stats_record_action()
+ * do per packet.  Stream-ordered on @stream (hipStream_t or NULL).
+ */
+int xfg_classify(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
+		 uint8_t *verdicts, void *stream);
+
+/*
+ * Host-resident batch: copies packets to the device (pinned staging,
+ * pipelined H2D / kernel / D2H over chunks), classifies, copies verdicts
+ * back.  Packet layout as struct xfg_batch but in host memory.
+ */
+int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
+		      uint8_t *verdicts);
+
+/* Per-action stats summed over devices (the userspace per-CPU sum of
+ * lib/util/stats.c:140-172), or for one device. */
+int xfg_stats_read(xfg_ctx *ctx, struct xfg_stats_record out[XFG_ACTION_MAX]);
+int xfg_stats_read_dev(xfg_ctx *ctx, int dev, struct xfg_stats_record out[XFG_ACTION_MAX]);
+int xfg_stats_reset(xfg_ctx *ctx);
+
+/* Wait for all work queued by this library on every device. */
+int xfg_sync(xfg_ctx *ctx);
+
+/* ---- device memory helpers (so a C host needs no HIP headers) ---- */
+void *xfg_dev_alloc(xfg_ctx *ctx, int dev, size_t bytes);
+void xfg_dev_free(xfg_ctx *ctx, int dev, void *p);
+int xfg_memcpy_h2d(xfg_ctx *ctx, int dev, void *dst, const void *src, size_t bytes);
+int xfg_memcpy_d2h(xfg_ctx *ctx, int dev, void *dst, const void *src, size_t bytes);
+void *xfg_host_alloc_pinned(size_t bytes);
+void xfg_host_free_pinned(void *p);
+
+/* ---- timing: HIP events on the library's stream for device @dev ---- */
+/* Launch classify @iters times back-to-back on the device's stream and
+ * return the average kernel duration in ms measured with HIP events recorded
+ * on that same stream (used by bench.py for the roofline figure). */
+int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
+		       uint8_t *verdicts, int iters, double *avg_ms);
+
+/*
+ * Multi-process reduction over RCCL (one process per GPU, one device per
+ * context).  Rank 0 calls xfg_comm_unique_id() and distributes the 128-byte
+ * id out of band; every rank then calls xfg_comm_init().  xfg_comm_allreduce()
+ * sums per-rule hit counters and per-action stats across ranks (ncclUint64,
+ * ncclSum, in place on a reduction copy); afterwards xfg_map_lookup() /
+ * xfg_stats_read() on every rank return the job-wide totals until the next
+ * classify call.  This is the GPU analogue of summing per-CPU values
+ * (xdp-filter/xdp-filter.c:93-103).
+ */
+#define XFG_COMM_ID_BYTES 128
+int xfg_comm_unique_id(uint8_t id[XFG_COMM_ID_BYTES]);
+int xfg_comm_init(xfg_ctx *ctx, int nranks, int rank, const uint8_t id[XFG_COMM_ID_BYTES]);
+int xfg_comm_allreduce(xfg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XDPFILTER_GPU_H */
