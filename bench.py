@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark: Mpps classified (device-resident), 64B
+frames, xdpfilt_dny_all, 1M IPv4 rules (BASELINE.json configs[2] = "C3").
+
+One step = one xfg_classify() launch over the whole synthetic batch resident
+in HBM (2^24 packets of 64 B per GPU by default).  N GPUs = N processes, one
+per GPU, each with its own shard (rank-seeded batch; rule tables replicated):
+weak scaling, no data-path collective.  Counters are reduced over RCCL once,
+after the timed region (reported separately as reduce_ms).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+  roofline:     algorithmic bytes per launch (sum over packets of
+                min(len,128)+1) / average kernel duration from
+                HIP events on the launch stream, vs the 8 TB/s HBM peak
+  cpu_baseline: the reference program (oracle/_ref, host-compiled, 1 core)
+                on a bounded sample of the same workload (N=1, rank 0 only).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "xdp-tools_amd", "python"))
+
+METRIC = "Mpps classified (device-resident), 64B frames, xdpfilt_dny_all; 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log2-packets", type=int, default=24)
+    ap.add_argument("--rules", type=int, default=1_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU-baseline duration (0 disables)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: CPU barrier/max only
+        dist.init_process_group("gloo")
+    import numpy as np
+    import xftools as X
+    import xfgpu as G
+
+    n = 1 << args.log2_packets
+    stride = 64
+    # ---- rules: 1M IPv4 dst rules (seed 3) + 16 dst-port rules (tcp,udp)
+    v4 = X.rand_keys(3, int(args.rules * 1.02) + 16, 4)[:args.rules]
+    ports = (np.arange(16, dtype=np.uint16) * 1031 + 53).astype(np.uint16)
+    # ---- traffic: C3 mix, shard seeded by rank
+    t0 = time.time()
+    data, lens = X.gen_workload(3 + 1000 * rank, 3, n, stride, v4=v4, ports=ports,
+                                dst_permille=500, port_permille=250, bad_permille=10)
+    lens16 = lens.astype(np.uint16)
+    gen_s = time.time() - t0
+
+    f = G.Filter(G.FEAT_ALL | G.FEAT_DENY, devices=[local], ipv4_capacity=args.rules)
+    assert f.prog_name == "xdpfilt_dny_all"
+    f.update_batch(G.MAP_IPV4, v4, np.full(len(v4), 2, np.uint64))           # dst
+    pkeys = np.array([X.port_key(int(p)) for p in ports], "<u4").view(np.uint8)
+    f.update_batch(G.MAP_PORTS, pkeys, np.full(len(ports), 2 | 4 | 8, np.uint64))
+    d_data = f.alloc(data.nbytes)
+    d_data.upload(data)
+    d_lens = f.alloc(lens16.nbytes)
+    d_lens.upload(lens16)
+    d_verd = f.alloc(n)
+    del data
+
+    alg_bytes = int(np.minimum(lens.astype(np.int64), 128).sum() + n)   # min(len,128)+1
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    # ---- warmup
+    if args.warmup:
+        f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, args.warmup, lens_u16=True)
+    f.sync()
+    # ---- timed region: K launches back-to-back on the library's stream,
+    # HIP events recorded on that stream around them
+    barrier()
+    f.sync()
+    t1 = time.perf_counter()
+    kern_ms = f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, args.steps,
+                               lens_u16=True)
+    f.sync()
+    barrier()
+    wall = time.perf_counter() - t1
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    # ---- sanity on the run's own outputs (cheap, not a parity claim)
+    st = f.stats(dev=0)
+    assert int(st[:, 0].sum()) == n * (args.steps + args.warmup), st
+
+    # ---- RCCL counter reduce (once, after the timed region)
+    reduce_ms = None
+    if world > 1:
+        uid = [G.Filter.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        f.comm_init(world, rank, uid[0])
+        f.sync()
+        barrier()
+        tr = time.perf_counter()
+        f.comm_allreduce()
+        reduce_ms = (time.perf_counter() - tr) * 1e3
+
+    # ---- achievable streaming-read peak on this device (same 1 GiB buffer)
+    peak_meas_ms = f.stream_read_timed(d_data.ptr, n * stride, 5)
+    peak_meas = n * stride / (peak_meas_ms * 1e-3) / 1e9
+
+    # ---- CPU baseline (rank 0, N=1 only)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0:
+        cpu = cpu_baseline(X, np, v4, ports, args.cpu_seconds)
+
+    total_pkts = n * args.steps * world
+    value = total_pkts / wall / 1e6
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded xorshift64*, tools/xfsynth.c)",
+        "config": {
+            "workload": "C3: xdpfilt_dny_all, 1M IPv4 dst rules + 16 dst-port rules (tcp|udp), "
+                        "64B frames at 64B stride (80% IPv4/UDP, 10% IPv4/TCP, 10% IPv6/UDP 62B, "
+                        "1% malformed), 50% dst-IP hits, u16 lens, device-resident",
+            "packets_per_gpu": n,
+            "rules_ipv4": args.rules,
+            "program": f.prog_name,
+            "parallelism": f"shard{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "alg_bytes_per_launch": alg_bytes,
+            "kernel_ms": round(kern_ms, 4),
+            "peak_measured_stream_read": round(peak_meas, 1),
+            "frac_of_measured": round(achieved / peak_meas, 4),
+        },
+        "cpu_baseline": cpu,
+        "gen_seconds": round(gen_s, 2),
+    }
+    if reduce_ms is not None:
+        line["reduce_ms"] = round(reduce_ms, 3)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    f.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(X, np, v4, ports, seconds):
+    """The reference xdpfilt_dny_all (oracle/_ref, unmodified, host-compiled)
+    on one core over a 2^22-packet sample of the same workload, repeated
+    until ~`seconds` elapsed.  Falls back to the C restatement ("port") when
+    the reference build is absent."""
+    m = 1 << 22
+    stride = 64
+    libc = C.CDLL(None)
+    libc.mmap.restype = C.c_void_p
+    libc.mmap.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_long]
+    # MAP_PRIVATE|MAP_ANONYMOUS|MAP_32BIT: struct xdp_md carries 32-bit pointers
+    addr = libc.mmap(None, m * stride, 3, 0x02 | 0x20 | 0x40, -1, 0)
+    if addr in (None, C.c_void_p(-1).value):
+        buf = np.zeros(m * stride, np.uint8)
+    else:
+        buf = np.ctypeslib.as_array((C.c_uint8 * (m * stride)).from_address(addr))
+    lens = np.zeros(m, np.uint32)
+    X.gen_workload(3, 3, m, stride, v4=v4, ports=ports, data=buf, lens=lens)
+    rules = X.RuleSet()
+    rules.v4_keys = v4
+    rules.v4_vals = np.full(len(v4), 2, np.uint64)
+    for p in ports:
+        rules.ports[X.port_key(int(p))] = 2 | 4 | 8
+    kind = "reference" if X.ref_available() else "port"
+    rules = rules.prepared()
+    maps = None if kind == "reference" else X.OracleMaps(rules)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        if kind == "reference":   # index over the rule list is cached across passes
+            X.run_ref("xdpfilt_dny_all", buf, lens, rules, stride=stride, in_place=True)
+        else:
+            X.run_oracle(X.VARIANT_FEATURES["xdpfilt_dny_all"], buf, lens, rules, stride=stride,
+                         maps=maps)
+        done += m
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(done / el / 1e6, 2), "unit": "Mpps", "cores": 1, "kind": kind,
+            "sample": f"{done} packets ({done // m} passes over a 2^22-packet C3 sample, "
+                      f"1M IPv4 rules), 1 thread, {el:.1f}s, "
+                      f"{'oracle/_ref xdpfilt_dny_all' if kind == 'reference' else 'oracle restatement'}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -118,6 +118,11 @@ int xfg_map_delete(xfg_ctx *ctx, int map, const void *key);
 int xfg_map_get_next_key(xfg_ctx *ctx, int map, const void *key, void *next_key);
 /* Number of keys present (ports: number of non-zero entries). */
 int64_t xfg_map_count(xfg_ctx *ctx, int map);
+/* Bulk lookup of @n keys (status readout, parity checks): vals[i*ndev + d]
+ * receives device d's value of key i, present[i] (if not NULL) 1/0; absent
+ * keys read as 0.  Returns the number of keys found or a negative errno. */
+int64_t xfg_map_lookup_batch(xfg_ctx *ctx, int map, const void *keys, uint64_t n,
+			     uint64_t *vals, uint8_t *present);
 /* Bulk insert/overwrite of @n keys with the same value on every device
  * (rule-set loading).  Returns 0 or the first error (-E2BIG, ...). */
 int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t *vals,
@@ -182,6 +187,12 @@ void xfg_host_free_pinned(void *p);
  * on that same stream (used by bench.py for the roofline figure). */
 int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
 		       uint8_t *verdicts, int iters, double *avg_ms);
+
+/* Streaming-read probe: average duration of a kernel that reads @bytes of
+ * device memory at @src with 16-byte non-temporal loads (the achievable HBM
+ * read rate next to the spec peak, for the roofline report). */
+int xfg_stream_read_timed(xfg_ctx *ctx, int dev, const void *src, uint64_t bytes, int iters,
+			  double *avg_ms);
 
 /*
  * Multi-process reduction over RCCL (one process per GPU, one device per

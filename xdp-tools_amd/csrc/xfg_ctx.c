@@ -1,0 +1,1121 @@
+/* SPDX-License-Identifier: GPL-2.0 */
+/*
+ * xfg_ctx.c — host runtime behind include/xdpfilter_gpu.h (plain C over the
+ * HIP runtime C API; the kernels live in xfg_kernels.hip).
+ *
+ * What replaces what in the reference:
+ *   program selection     find_prog_file()          xdp-filter/xdp-filter.c:48-60
+ *   BPF map CRUD          bpf_map_*_elem() on pinned per-CPU maps
+ *                         (xdp-filter/xdp-filter.c:73-157; lib/util/util.h:29-33)
+ *   per-CPU value copies  one value per device (flags + hits arrays in HBM)
+ *   stats readout         map_get_value_percpu_array  lib/util/stats.c:140-172
+ *   prog_lock_acquire     a context mutex           lib/util/util.c:727-767
+ */
+#define _GNU_SOURCE
+#include "xdpfilter_gpu.h"
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "xfg_layout.h"
+#include "xfg_table.h"
+
+/* from xfg_kernels.hip */
+int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a, unsigned grid,
+			void *stream);
+int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sink, unsigned grid,
+			   void *stream);
+
+#define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
+
+struct dev_map {           /* device arrays of one hash map */
+	void *keys;
+	uint8_t *meta;
+	uint8_t *flags;
+	unsigned long long *hits;
+	unsigned long long *red_hits; /* reduction copy (multi-process) */
+};
+
+struct xfg_dev {
+	int ordinal;
+	int ncu;
+	hipStream_t stream;
+	hipEvent_t ev0, ev1;
+	struct dev_map m[NMAPS_HASH];
+	uint8_t *port_flags;
+	unsigned long long *port_hits;
+	unsigned long long *red_port_hits;
+	unsigned long long *stats;      /* 10 */
+	unsigned long long *red_stats;  /* 10 */
+	void *sink;                     /* stream-read probe sink */
+};
+
+struct xfg_ctx {
+	pthread_mutex_t lock;
+	uint32_t prog_features;
+	const char *prog_name;
+	int ndev;
+	struct xfg_dev *dev;
+	struct xfg_table t[NMAPS_HASH];  /* index = map id - 1 */
+	/* host-only context: value store for ndev == 0 */
+	uint64_t *host_vals[NMAPS_HASH];
+	uint64_t *host_port_vals;
+	uint8_t *port_flags_host;        /* flags of device 0 view (for port_count) */
+	uint32_t port_count;
+	/* multi-process reduction */
+	ncclComm_t comm;
+	int comm_ready;
+	int reduced;
+};
+
+/* ------------------------------------------------------------------ misc */
+static const struct { const char *name; uint32_t feat; } prog_table[] = {
+	/* xdp-filter/Makefile:3-6 order; features = each program's _features */
+	{ "xdpfilt_dny_udp", XFG_FEAT_UDP | XFG_FEAT_DENY },
+	{ "xdpfilt_dny_tcp", XFG_FEAT_TCP | XFG_FEAT_DENY },
+	{ "xdpfilt_dny_ip", XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_DENY },
+	{ "xdpfilt_dny_eth", XFG_FEAT_ETHERNET | XFG_FEAT_DENY },
+	{ "xdpfilt_dny_all", XFG_FEAT_ALL | XFG_FEAT_DENY },
+	{ "xdpfilt_alw_udp", XFG_FEAT_UDP | XFG_FEAT_ALLOW },
+	{ "xdpfilt_alw_tcp", XFG_FEAT_TCP | XFG_FEAT_ALLOW },
+	{ "xdpfilt_alw_ip", XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_ALLOW },
+	{ "xdpfilt_alw_eth", XFG_FEAT_ETHERNET | XFG_FEAT_ALLOW },
+	{ "xdpfilt_alw_all", XFG_FEAT_ALL | XFG_FEAT_ALLOW },
+};
+
+int xfg_select_program(uint32_t features, const char **prog_name, uint32_t *prog_features)
+{
+	if (!features)
+		return -EINVAL;
+	for (size_t i = 0; i < sizeof(prog_table) / sizeof(prog_table[0]); i++) {
+		if ((prog_table[i].feat & features) == features) {
+			if (prog_name)
+				*prog_name = prog_table[i].name;
+			if (prog_features)
+				*prog_features = prog_table[i].feat;
+			return 0;
+		}
+	}
+	return -ENOENT;
+}
+
+const char *xfg_strerror(int err)
+{
+	if (err <= -1000)
+		return "HIP runtime error";
+	return strerror(err < 0 ? -err : err);
+}
+
+static int hip_err(hipError_t e)
+{
+	if (e == hipSuccess)
+		return 0;
+	if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+		return -ENOMEM;
+	if (e == hipErrorNoDevice || e == hipErrorInvalidDevice)
+		return -ENODEV;
+	return -1000 - (int)e;
+}
+
+#define HIPCHK(call)                                  \
+	do {                                          \
+		int _e = hip_err(call);               \
+		if (_e) {                             \
+			err = _e;                     \
+			goto fail;                    \
+		}                                     \
+	} while (0)
+
+static int keylen_of(int map)
+{
+	switch (map) {
+	case XFG_MAP_PORTS: return 4;
+	case XFG_MAP_IPV4: return 4;
+	case XFG_MAP_IPV6: return 16;
+	case XFG_MAP_ETHERNET: return 6;
+	default: return -EINVAL;
+	}
+}
+
+/* ------------------------------------------------------------------ open */
+static void dev_free(struct xfg_dev *d)
+{
+	if (hipSetDevice(d->ordinal) != hipSuccess)
+		return;
+	for (int i = 0; i < NMAPS_HASH; i++) {
+		hipFree(d->m[i].keys);
+		hipFree(d->m[i].meta);
+		hipFree(d->m[i].flags);
+		hipFree(d->m[i].hits);
+		hipFree(d->m[i].red_hits);
+	}
+	hipFree(d->port_flags);
+	hipFree(d->port_hits);
+	hipFree(d->red_port_hits);
+	hipFree(d->stats);
+	hipFree(d->red_stats);
+	hipFree(d->sink);
+	if (d->ev0)
+		hipEventDestroy(d->ev0);
+	if (d->ev1)
+		hipEventDestroy(d->ev1);
+	if (d->stream)
+		hipStreamDestroy(d->stream);
+}
+
+static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
+{
+	int err = 0;
+	hipDeviceProp_t prop;
+
+	HIPCHK(hipSetDevice(d->ordinal));
+	HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
+	d->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+	HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+	HIPCHK(hipEventCreate(&d->ev0));
+	HIPCHK(hipEventCreate(&d->ev1));
+	for (int i = 0; i < NMAPS_HASH; i++) {
+		const struct xfg_table *t = &ctx->t[i];
+		size_t ns = (size_t)t->nslots + 1;
+		HIPCHK(hipMalloc(&d->m[i].keys, (size_t)t->nbuckets * XFG_BUCKET_BYTES));
+		HIPCHK(hipMalloc((void **)&d->m[i].meta, t->nbuckets));
+		HIPCHK(hipMalloc((void **)&d->m[i].flags, ns));
+		HIPCHK(hipMalloc((void **)&d->m[i].hits, ns * 8));
+		HIPCHK(hipMemset(d->m[i].keys, 0, (size_t)t->nbuckets * XFG_BUCKET_BYTES));
+		HIPCHK(hipMemset(d->m[i].meta, 0, t->nbuckets));
+		HIPCHK(hipMemset(d->m[i].flags, 0, ns));
+		HIPCHK(hipMemset(d->m[i].hits, 0, ns * 8));
+	}
+	HIPCHK(hipMalloc((void **)&d->port_flags, XFG_PORT_MAP_ENTRIES));
+	HIPCHK(hipMalloc((void **)&d->port_hits, XFG_PORT_MAP_ENTRIES * 8));
+	HIPCHK(hipMemset(d->port_flags, 0, XFG_PORT_MAP_ENTRIES));
+	HIPCHK(hipMemset(d->port_hits, 0, XFG_PORT_MAP_ENTRIES * 8));
+	HIPCHK(hipMalloc((void **)&d->stats, 10 * 8));
+	HIPCHK(hipMemset(d->stats, 0, 10 * 8));
+	HIPCHK(hipMalloc(&d->sink, 16 * 65536));
+	HIPCHK(hipDeviceSynchronize());
+	return 0;
+fail:
+	return err;
+}
+
+int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
+{
+	int err;
+	xfg_ctx *ctx;
+
+	if (!out || !opts)
+		return -EINVAL;
+	*out = NULL;
+	ctx = calloc(1, sizeof(*ctx));
+	if (!ctx)
+		return -ENOMEM;
+	pthread_mutex_init(&ctx->lock, NULL);
+	err = xfg_select_program(opts->features, &ctx->prog_name, &ctx->prog_features);
+	if (err)
+		goto fail;
+
+	uint32_t seed = opts->hash_seed ? opts->hash_seed : 0x5eed1234u;
+	uint32_t cap4 = opts->ipv4_capacity ? opts->ipv4_capacity : XFG_DEFAULT_MAP_CAPACITY;
+	uint32_t cap6 = opts->ipv6_capacity ? opts->ipv6_capacity : XFG_DEFAULT_MAP_CAPACITY;
+	uint32_t cape = opts->eth_capacity ? opts->eth_capacity : XFG_DEFAULT_MAP_CAPACITY;
+	if ((err = xfg_table_init(&ctx->t[0], 4, cap4, seed)) ||
+	    (err = xfg_table_init(&ctx->t[1], 16, cap6, seed ^ 0x6a09e667u)) ||
+	    (err = xfg_table_init(&ctx->t[2], 6, cape, seed ^ 0xbb67ae85u)))
+		goto fail;
+	ctx->port_flags_host = calloc(XFG_PORT_MAP_ENTRIES, 1);
+	if (!ctx->port_flags_host) {
+		err = -ENOMEM;
+		goto fail;
+	}
+
+	ctx->ndev = opts->ndev > 0 ? opts->ndev : 0;
+	if (!ctx->ndev) {
+		for (int i = 0; i < NMAPS_HASH; i++) {
+			ctx->host_vals[i] = calloc((size_t)ctx->t[i].nslots + 1, 8);
+			if (!ctx->host_vals[i]) {
+				err = -ENOMEM;
+				goto fail;
+			}
+		}
+		ctx->host_port_vals = calloc(XFG_PORT_MAP_ENTRIES, 8);
+		if (!ctx->host_port_vals) {
+			err = -ENOMEM;
+			goto fail;
+		}
+	} else {
+		int count = 0;
+		if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+			err = -ENODEV;
+			goto fail;
+		}
+		ctx->dev = calloc(ctx->ndev, sizeof(*ctx->dev));
+		if (!ctx->dev) {
+			err = -ENOMEM;
+			goto fail;
+		}
+		for (int i = 0; i < ctx->ndev; i++) {
+			ctx->dev[i].ordinal = opts->devices ? opts->devices[i] : i;
+			if (ctx->dev[i].ordinal < 0 || ctx->dev[i].ordinal >= count) {
+				err = -ENODEV;
+				goto fail;
+			}
+			if ((err = dev_init(ctx, &ctx->dev[i])))
+				goto fail;
+		}
+	}
+	*out = ctx;
+	return 0;
+fail:
+	xfg_close(ctx);
+	return err;
+}
+
+void xfg_close(xfg_ctx *ctx)
+{
+	if (!ctx)
+		return;
+	if (ctx->comm_ready)
+		ncclCommDestroy(ctx->comm);
+	for (int i = 0; i < ctx->ndev && ctx->dev; i++)
+		dev_free(&ctx->dev[i]);
+	free(ctx->dev);
+	for (int i = 0; i < NMAPS_HASH; i++) {
+		xfg_table_free(&ctx->t[i]);
+		free(ctx->host_vals[i]);
+	}
+	free(ctx->host_port_vals);
+	free(ctx->port_flags_host);
+	pthread_mutex_destroy(&ctx->lock);
+	free(ctx);
+}
+
+const char *xfg_prog_name(const xfg_ctx *ctx) { return ctx ? ctx->prog_name : NULL; }
+uint32_t xfg_prog_features(const xfg_ctx *ctx) { return ctx ? ctx->prog_features : 0; }
+int xfg_num_devices(const xfg_ctx *ctx) { return ctx ? ctx->ndev : -EINVAL; }
+
+/* ------------------------------------------------------------------ maps */
+static int dev_read(struct xfg_dev *d, void *dst, const void *src, size_t n)
+{
+	int err = hip_err(hipSetDevice(d->ordinal));
+	if (!err)
+		err = hip_err(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, d->stream));
+	if (!err)
+		err = hip_err(hipStreamSynchronize(d->stream));
+	return err;
+}
+
+static int dev_write(struct xfg_dev *d, void *dst, const void *src, size_t n)
+{
+	int err = hip_err(hipSetDevice(d->ordinal));
+	if (!err)
+		err = hip_err(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, d->stream));
+	if (!err)
+		err = hip_err(hipStreamSynchronize(d->stream));
+	return err;
+}
+
+/* Read the per-device values of @slot of hash map @mi (0..2). */
+static int slot_values(xfg_ctx *ctx, int mi, uint64_t slot, uint64_t *vals)
+{
+	if (!ctx->ndev) {
+		vals[0] = ctx->host_vals[mi][slot];
+		return 0;
+	}
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		uint8_t f;
+		unsigned long long h;
+		int err = dev_read(d, &f, d->m[mi].flags + slot, 1);
+		if (!err)
+			err = dev_read(d, &h, (ctx->reduced ? d->m[mi].red_hits : d->m[mi].hits) + slot, 8);
+		if (err)
+			return err;
+		vals[i] = (h << XFG_COUNTER_SHIFT) | f;
+	}
+	return 0;
+}
+
+static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals)
+{
+	if (!ctx->ndev) {
+		ctx->host_vals[mi][slot] = vals[0];
+		return 0;
+	}
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		uint8_t f = vals[i] & 63;
+		unsigned long long h = vals[i] >> XFG_COUNTER_SHIFT;
+		int err = dev_write(d, d->m[mi].flags + slot, &f, 1);
+		if (!err)
+			err = dev_write(d, d->m[mi].hits + slot, &h, 8);
+		if (err)
+			return err;
+	}
+	return 0;
+}
+
+/* Push the key image of bucket @b of map @mi to every device. */
+static int push_bucket(xfg_ctx *ctx, int mi, uint32_t b)
+{
+	const struct xfg_table *t = &ctx->t[mi];
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		int err = dev_write(d, (uint8_t *)d->m[mi].keys + (size_t)b * XFG_BUCKET_BYTES,
+				    t->keys + (size_t)b * XFG_BUCKET_BYTES, XFG_BUCKET_BYTES);
+		if (err)
+			return err;
+	}
+	return 0;
+}
+
+struct meta_push { xfg_ctx *ctx; int mi; int err; };
+
+static void meta_changed(void *arg, uint32_t b)
+{
+	struct meta_push *mp = arg;
+	xfg_ctx *ctx = mp->ctx;
+	for (int i = 0; i < ctx->ndev && !mp->err; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		mp->err = dev_write(d, d->m[mp->mi].meta + b, ctx->t[mp->mi].meta + b, 1);
+	}
+}
+
+static int port_key(const void *key, uint32_t *k)
+{
+	memcpy(k, key, 4);
+	return *k < XFG_PORT_MAP_ENTRIES ? 0 : -ENOENT;
+}
+
+static void port_flags_note(xfg_ctx *ctx, uint32_t k, uint8_t f)
+{
+	if (!ctx->port_flags_host[k] && f)
+		ctx->port_count++;
+	else if (ctx->port_flags_host[k] && !f)
+		ctx->port_count--;
+	ctx->port_flags_host[k] = f;
+}
+
+int xfg_map_lookup(xfg_ctx *ctx, int map, const void *key, uint64_t *vals)
+{
+	int err = 0;
+	if (!ctx || !key || !vals || keylen_of(map) < 0)
+		return -EINVAL;
+	pthread_mutex_lock(&ctx->lock);
+	if (map == XFG_MAP_PORTS) {
+		uint32_t k;
+		if ((err = port_key(key, &k)))
+			goto out;
+		if (!ctx->ndev) {
+			vals[0] = ctx->host_port_vals[k];
+			goto out;
+		}
+		for (int i = 0; i < ctx->ndev && !err; i++) {
+			struct xfg_dev *d = &ctx->dev[i];
+			uint8_t f;
+			unsigned long long h;
+			err = dev_read(d, &f, d->port_flags + k, 1);
+			if (!err)
+				err = dev_read(d, &h, (ctx->reduced ? d->red_port_hits : d->port_hits) + k, 8);
+			vals[i] = (h << XFG_COUNTER_SHIFT) | f;
+		}
+		goto out;
+	}
+	int mi = map - 1;
+	int64_t s = xfg_table_find(&ctx->t[mi], key);
+	if (s < 0) {
+		err = -ENOENT;
+		goto out;
+	}
+	err = slot_values(ctx, mi, (uint64_t)s, vals);
+out:
+	pthread_mutex_unlock(&ctx->lock);
+	return err;
+}
+
+int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals)
+{
+	int err = 0;
+	if (!ctx || !key || !vals || keylen_of(map) < 0)
+		return -EINVAL;
+	pthread_mutex_lock(&ctx->lock);
+	ctx->reduced = 0;
+	if (map == XFG_MAP_PORTS) {
+		uint32_t k;
+		if ((err = port_key(key, &k))) {
+			err = -E2BIG; /* array map: index out of range */
+			goto out;
+		}
+		if (!ctx->ndev) {
+			ctx->host_port_vals[k] = vals[0];
+			port_flags_note(ctx, k, vals[0] & 63);
+			goto out;
+		}
+		for (int i = 0; i < ctx->ndev && !err; i++) {
+			struct xfg_dev *d = &ctx->dev[i];
+			uint8_t f = vals[i] & 63;
+			unsigned long long h = vals[i] >> XFG_COUNTER_SHIFT;
+			err = dev_write(d, d->port_flags + k, &f, 1);
+			if (!err)
+				err = dev_write(d, d->port_hits + k, &h, 8);
+		}
+		/* a port is "present" for the skip test if any device has flags */
+		{
+			uint8_t any = 0;
+			for (int i = 0; i < ctx->ndev; i++)
+				any |= vals[i] & 63;
+			port_flags_note(ctx, k, any);
+		}
+		goto out;
+	}
+	int mi = map - 1;
+	struct xfg_table *t = &ctx->t[mi];
+	int64_t s = xfg_table_find(t, key);
+	if (s < 0) {
+		struct meta_push mp = { ctx, mi, 0 };
+		s = xfg_table_insert(t, key, ctx->ndev ? meta_changed : NULL, &mp);
+		if (s < 0) {
+			err = (int)s;
+			goto out;
+		}
+		if ((err = mp.err))
+			goto out;
+		if ((uint64_t)s != t->nslots && ctx->ndev)
+			err = push_bucket(ctx, mi, (uint32_t)(s / t->slots_per_bucket));
+		if (err)
+			goto out;
+	}
+	err = slot_store(ctx, mi, (uint64_t)s, vals);
+out:
+	pthread_mutex_unlock(&ctx->lock);
+	return err;
+}
+
+int xfg_map_delete(xfg_ctx *ctx, int map, const void *key)
+{
+	int err = 0;
+	if (!ctx || !key || keylen_of(map) < 0)
+		return -EINVAL;
+	if (map == XFG_MAP_PORTS)
+		return -EINVAL; /* BPF array maps do not support delete */
+	pthread_mutex_lock(&ctx->lock);
+	int mi = map - 1;
+	struct xfg_table *t = &ctx->t[mi];
+	int64_t s = xfg_table_remove(t, key);
+	if (s < 0) {
+		err = (int)s;
+		goto out;
+	}
+	{
+		uint64_t zero[64] = { 0 };
+		uint64_t *z = ctx->ndev > 64 ? calloc(ctx->ndev, 8) : zero;
+		if (!z) {
+			err = -ENOMEM;
+			goto out;
+		}
+		err = slot_store(ctx, mi, (uint64_t)s, z);
+		if (z != zero)
+			free(z);
+	}
+	if (!err && (uint64_t)s != t->nslots && ctx->ndev)
+		err = push_bucket(ctx, mi, (uint32_t)(s / t->slots_per_bucket));
+out:
+	pthread_mutex_unlock(&ctx->lock);
+	return err;
+}
+
+int xfg_map_get_next_key(xfg_ctx *ctx, int map, const void *key, void *next_key)
+{
+	int err = 0;
+	if (!ctx || !next_key || keylen_of(map) < 0)
+		return -EINVAL;
+	if (map == XFG_MAP_PORTS) {
+		/* BPF array semantics: next index; a missing/invalid key restarts at 0 */
+		uint32_t k = 0;
+		if (key) {
+			memcpy(&k, key, 4);
+			if (k >= XFG_PORT_MAP_ENTRIES)
+				k = 0;
+			else if (k + 1 >= XFG_PORT_MAP_ENTRIES)
+				return -ENOENT;
+			else
+				k++;
+		}
+		memcpy(next_key, &k, 4);
+		return 0;
+	}
+	pthread_mutex_lock(&ctx->lock);
+	const struct xfg_table *t = &ctx->t[map - 1];
+	int64_t after = -1;
+	if (key) {
+		int64_t s = xfg_table_find(t, key);
+		after = s; /* BPF htab: a missing key restarts at the first key */
+	}
+	int64_t s = xfg_table_next_slot(t, after);
+	if (s < 0)
+		err = -ENOENT;
+	else
+		err = xfg_table_slot_key(t, (uint64_t)s, next_key);
+	pthread_mutex_unlock(&ctx->lock);
+	return err;
+}
+
+int64_t xfg_map_count(xfg_ctx *ctx, int map)
+{
+	if (!ctx || keylen_of(map) < 0)
+		return -EINVAL;
+	if (map == XFG_MAP_PORTS)
+		return ctx->port_count;
+	return ctx->t[map - 1].count;
+}
+
+int64_t xfg_map_lookup_batch(xfg_ctx *ctx, int map, const void *keys, uint64_t n,
+			     uint64_t *vals, uint8_t *present)
+{
+	int err = 0, kl = keylen_of(map);
+	int64_t found = 0;
+	if (!ctx || (!keys && n) || (!vals && n) || kl < 0)
+		return -EINVAL;
+	int nd = ctx->ndev ? ctx->ndev : 1;
+	size_t ns = map == XFG_MAP_PORTS ? XFG_PORT_MAP_ENTRIES
+					 : (size_t)ctx->t[map - 1].nslots + 1;
+	uint8_t *flags = NULL;
+	unsigned long long *hits = NULL;
+	pthread_mutex_lock(&ctx->lock);
+	if (ctx->ndev) {
+		flags = malloc(ns * nd);
+		hits = malloc(ns * 8 * nd);
+		if (!flags || !hits) {
+			err = -ENOMEM;
+			goto out;
+		}
+		for (int i = 0; i < ctx->ndev && !err; i++) {
+			struct xfg_dev *d = &ctx->dev[i];
+			const uint8_t *fsrc = map == XFG_MAP_PORTS ? d->port_flags : d->m[map - 1].flags;
+			const unsigned long long *hsrc =
+				map == XFG_MAP_PORTS ? (ctx->reduced ? d->red_port_hits : d->port_hits)
+						     : (ctx->reduced ? d->m[map - 1].red_hits : d->m[map - 1].hits);
+			err = dev_read(d, flags + ns * i, fsrc, ns);
+			if (!err)
+				err = dev_read(d, hits + ns * i, hsrc, ns * 8);
+		}
+		if (err)
+			goto out;
+	}
+	for (uint64_t i = 0; i < n; i++) {
+		const uint8_t *k = (const uint8_t *)keys + (size_t)kl * i;
+		int64_t s;
+		if (map == XFG_MAP_PORTS) {
+			uint32_t pk;
+			s = port_key(k, &pk) ? -1 : (int64_t)pk;
+		} else {
+			s = xfg_table_find(&ctx->t[map - 1], k);
+		}
+		if (present)
+			present[i] = s >= 0;
+		for (int d = 0; d < nd; d++) {
+			uint64_t v = 0;
+			if (s >= 0) {
+				if (!ctx->ndev)
+					v = map == XFG_MAP_PORTS ? ctx->host_port_vals[s]
+								 : ctx->host_vals[map - 1][s];
+				else
+					v = (hits[ns * d + s] << XFG_COUNTER_SHIFT) | flags[ns * d + s];
+			}
+			vals[i * nd + d] = v;
+		}
+		found += s >= 0;
+	}
+out:
+	free(flags);
+	free(hits);
+	pthread_mutex_unlock(&ctx->lock);
+	return err ? err : found;
+}
+
+int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t *vals,
+			 uint64_t n)
+{
+	int err = 0, kl = keylen_of(map);
+	if (!ctx || (!keys && n) || (!vals && n) || kl < 0)
+		return -EINVAL;
+	if (map == XFG_MAP_PORTS) {
+		for (uint64_t i = 0; i < n && !err; i++) {
+			uint64_t v[64];
+			uint64_t *vv = ctx->ndev > 64 ? calloc(ctx->ndev, 8) : v;
+			if (!vv)
+				return -ENOMEM;
+			for (int d = 0; d < (ctx->ndev ? ctx->ndev : 1); d++)
+				vv[d] = vals[i];
+			err = xfg_map_update(ctx, map, (const uint8_t *)keys + 4 * i, vv);
+			if (vv != v)
+				free(vv);
+		}
+		return err;
+	}
+	pthread_mutex_lock(&ctx->lock);
+	ctx->reduced = 0;
+	int mi = map - 1;
+	struct xfg_table *t = &ctx->t[mi];
+	size_t ns = (size_t)t->nslots + 1;
+	uint8_t *flags = NULL;
+	unsigned long long *hits = NULL;
+	int nd = ctx->ndev ? ctx->ndev : 1;
+
+	if (ctx->ndev) {
+		flags = malloc(ns * nd);
+		hits = malloc(ns * 8 * nd);
+		if (!flags || !hits) {
+			err = -ENOMEM;
+			goto out;
+		}
+		for (int i = 0; i < ctx->ndev && !err; i++) {
+			struct xfg_dev *d = &ctx->dev[i];
+			if (t->count) {
+				err = dev_read(d, flags + ns * i, d->m[mi].flags, ns);
+				if (!err)
+					err = dev_read(d, hits + ns * i, d->m[mi].hits, ns * 8);
+			} else {
+				memset(flags + ns * i, 0, ns);
+				memset(hits + ns * i, 0, ns * 8);
+			}
+		}
+		if (err)
+			goto out;
+	}
+	for (uint64_t i = 0; i < n; i++) {
+		const uint8_t *k = (const uint8_t *)keys + (size_t)kl * i;
+		int64_t s = xfg_table_find(t, k);
+		if (s < 0)
+			s = xfg_table_insert(t, k, NULL, NULL);
+		if (s < 0) {
+			err = (int)s;
+			break;
+		}
+		if (ctx->ndev) {
+			for (int d = 0; d < nd; d++) {
+				flags[ns * d + s] = vals[i] & 63;
+				hits[ns * d + s] = vals[i] >> XFG_COUNTER_SHIFT;
+			}
+		} else {
+			ctx->host_vals[mi][s] = vals[i];
+		}
+	}
+	/* upload full images (also on partial failure: keys inserted so far stay) */
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		int e2 = dev_write(d, d->m[mi].keys, t->keys, (size_t)t->nbuckets * XFG_BUCKET_BYTES);
+		if (!e2)
+			e2 = dev_write(d, d->m[mi].meta, t->meta, t->nbuckets);
+		if (!e2)
+			e2 = dev_write(d, d->m[mi].flags, flags + ns * i, ns);
+		if (!e2)
+			e2 = dev_write(d, d->m[mi].hits, hits + ns * i, ns * 8);
+		if (e2 && !err)
+			err = e2;
+	}
+out:
+	free(flags);
+	free(hits);
+	pthread_mutex_unlock(&ctx->lock);
+	return err;
+}
+
+/* ------------------------------------------------------------------ classify */
+static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b,
+		       uint8_t *verdicts, struct xfg_kargs *a)
+{
+	memset(a, 0, sizeof(*a));
+	struct xfg_tdesc *td[NMAPS_HASH] = { &a->t4, &a->t6, &a->te };
+	for (int i = 0; i < NMAPS_HASH; i++) {
+		xfg_table_desc(&ctx->t[i], td[i]);
+		td[i]->keys = d->m[i].keys;
+		td[i]->meta = d->m[i].meta;
+		td[i]->flags = d->m[i].flags;
+		td[i]->hits = d->m[i].hits;
+	}
+	a->port_flags = d->port_flags;
+	a->port_hits = d->port_hits;
+	a->port_count = ctx->port_count;
+	a->stats = d->stats;
+	a->data = b->data;
+	a->offsets = b->offsets;
+	a->lens = b->lens;
+	a->n = b->count;
+	a->stride = b->stride;
+	a->lens_u16 = b->lens_u16;
+	a->verdicts = verdicts;
+	/* Header window: the fixed-stride 64-byte layout needs no more than its
+	 * stride; everything else stages 128 bytes (every synthetic class and all
+	 * common headers parse within 78 bytes; longer chains read HBM). */
+	a->window = (!b->offsets && b->stride && b->stride <= 64) ? 64 : 128;
+}
+
+static unsigned grid_for(const struct xfg_dev *d, uint64_t n)
+{
+	uint64_t tiles = (n + 255) / 256;
+	uint64_t cap = (uint64_t)d->ncu * 8;
+	if (tiles > cap)
+		tiles = cap;
+	return tiles ? (unsigned)tiles : 1;
+}
+
+static int check_batch(xfg_ctx *ctx, int dev, const struct xfg_batch *b, const void *verdicts)
+{
+	if (!ctx || !b || (!verdicts && b->count))
+		return -EINVAL;
+	if (!ctx->ndev)
+		return -ENODEV;
+	if (dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	if (b->count && (!b->data || !b->lens))
+		return -EINVAL;
+	if (!b->offsets && b->count && (b->stride == 0 || (b->stride & 15)))
+		return -EINVAL;
+	if (((uintptr_t)b->data & 15))
+		return -EINVAL;
+	return 0;
+}
+
+int xfg_classify(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verdicts,
+		 void *stream)
+{
+	int err = check_batch(ctx, dev, b, verdicts);
+	if (err)
+		return err;
+	if (!b->count)
+		return 0;
+	struct xfg_dev *d = &ctx->dev[dev];
+	struct xfg_kargs a;
+	pthread_mutex_lock(&ctx->lock);
+	ctx->reduced = 0;
+	fill_kargs(ctx, d, b, verdicts, &a);
+	pthread_mutex_unlock(&ctx->lock);
+	err = hip_err(hipSetDevice(d->ordinal));
+	if (!err)
+		err = xfg_launch_classify(ctx->prog_features, &a, grid_for(d, b->count),
+					  stream ? stream : (void *)d->stream);
+	return err;
+}
+
+int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verdicts,
+		       int iters, double *avg_ms)
+{
+	int err = check_batch(ctx, dev, b, verdicts);
+	if (err)
+		return err;
+	if (iters < 1 || !avg_ms)
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[dev];
+	struct xfg_kargs a;
+	float ms = 0;
+	pthread_mutex_lock(&ctx->lock);
+	ctx->reduced = 0;
+	fill_kargs(ctx, d, b, verdicts, &a);
+	pthread_mutex_unlock(&ctx->lock);
+	unsigned grid = grid_for(d, b->count);
+	HIPCHK(hipSetDevice(d->ordinal));
+	HIPCHK(hipEventRecord(d->ev0, d->stream));
+	for (int i = 0; i < iters; i++) {
+		err = xfg_launch_classify(ctx->prog_features, &a, grid, d->stream);
+		if (err)
+			goto fail;
+	}
+	HIPCHK(hipEventRecord(d->ev1, d->stream));
+	HIPCHK(hipEventSynchronize(d->ev1));
+	HIPCHK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
+	*avg_ms = ms / iters;
+	return 0;
+fail:
+	return err;
+}
+
+/* Achievable streaming-read rate of the device (bench.py roofline leg). */
+int xfg_stream_read_timed(xfg_ctx *ctx, int dev, const void *src, uint64_t bytes, int iters,
+			  double *avg_ms)
+{
+	int err = 0;
+	float ms = 0;
+	if (!ctx || dev < 0 || dev >= ctx->ndev || !avg_ms || iters < 1)
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[dev];
+	unsigned grid = (unsigned)d->ncu * 8;
+	HIPCHK(hipSetDevice(d->ordinal));
+	HIPCHK(hipEventRecord(d->ev0, d->stream));
+	for (int i = 0; i < iters; i++)
+		if ((err = xfg_launch_stream_read(src, bytes, d->sink, grid, d->stream)))
+			goto fail;
+	HIPCHK(hipEventRecord(d->ev1, d->stream));
+	HIPCHK(hipEventSynchronize(d->ev1));
+	HIPCHK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
+	*avg_ms = ms / iters;
+	return 0;
+fail:
+	return err;
+}
+
+/* Host-resident batch: pinned double-buffered staging, H2D / kernel / D2H
+ * pipelined over two streams.  Whole frames cross PCIe (re-packed at a fixed
+ * 16-byte-aligned stride): a verdict may depend on bytes past any fixed
+ * header window (long IPv6 extension chains, TCP doff bounds checks against
+ * the full length), see DESIGN.md "host-resident rate". */
+int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verdicts)
+{
+	int err = 0;
+	if (!ctx || !b || (!verdicts && b->count))
+		return -EINVAL;
+	if (!ctx->ndev)
+		return -ENODEV;
+	if (dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	if (!b->count)
+		return 0;
+	struct xfg_dev *d = &ctx->dev[dev];
+	const uint64_t CH = 1u << 18;   /* packets per chunk */
+	uint64_t maxlen = 0;
+	for (uint64_t i = 0; i < b->count; i++) {
+		uint64_t l = b->lens_u16 ? ((const uint16_t *)b->lens)[i] : ((const uint32_t *)b->lens)[i];
+		if (l > maxlen)
+			maxlen = l;
+	}
+	uint32_t stride = (uint32_t)((maxlen + 15) & ~15ull);
+	if (stride < 64)
+		stride = 64;
+	size_t chunk_bytes = (size_t)CH * stride;
+	uint8_t *hbuf[2] = { NULL, NULL }, *dbuf[2] = { NULL, NULL }, *dv[2] = { NULL, NULL };
+	uint32_t *hl[2] = { NULL, NULL }, *dl[2] = { NULL, NULL };
+	hipStream_t st[2] = { NULL, NULL };
+	hipEvent_t done[2] = { NULL, NULL };
+
+	HIPCHK(hipSetDevice(d->ordinal));
+	for (int k = 0; k < 2; k++) {
+		HIPCHK(hipHostMalloc((void **)&hbuf[k], chunk_bytes, hipHostMallocDefault));
+		HIPCHK(hipHostMalloc((void **)&hl[k], CH * 4, hipHostMallocDefault));
+		HIPCHK(hipMalloc((void **)&dbuf[k], chunk_bytes));
+		HIPCHK(hipMalloc((void **)&dl[k], CH * 4));
+		HIPCHK(hipMalloc((void **)&dv[k], CH));
+		HIPCHK(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
+		HIPCHK(hipEventCreate(&done[k]));
+	}
+	for (uint64_t c = 0, k = 0; c < b->count; c += CH, k ^= 1) {
+		uint64_t m = b->count - c < CH ? b->count - c : CH;
+		HIPCHK(hipEventSynchronize(done[k]));   /* staging buffer k free again */
+		for (uint64_t i = 0; i < m; i++) {
+			uint64_t gi = c + i;
+			uint32_t l = b->lens_u16 ? ((const uint16_t *)b->lens)[gi] : ((const uint32_t *)b->lens)[gi];
+			const uint8_t *src = (const uint8_t *)b->data +
+					     (b->offsets ? b->offsets[gi] : gi * (uint64_t)b->stride);
+			memcpy(hbuf[k] + i * stride, src, l);
+			hl[k][i] = l;
+		}
+		HIPCHK(hipMemcpyAsync(dbuf[k], hbuf[k], m * stride, hipMemcpyHostToDevice, st[k]));
+		HIPCHK(hipMemcpyAsync(dl[k], hl[k], m * 4, hipMemcpyHostToDevice, st[k]));
+		struct xfg_batch sub = { dbuf[k], NULL, dl[k], m, stride, 0 };
+		struct xfg_kargs a;
+		pthread_mutex_lock(&ctx->lock);
+		ctx->reduced = 0;
+		fill_kargs(ctx, d, &sub, dv[k], &a);
+		pthread_mutex_unlock(&ctx->lock);
+		if ((err = xfg_launch_classify(ctx->prog_features, &a, grid_for(d, m), st[k])))
+			goto fail;
+		HIPCHK(hipMemcpyAsync(verdicts + c, dv[k], m, hipMemcpyDeviceToHost, st[k]));
+		HIPCHK(hipEventRecord(done[k], st[k]));
+	}
+	HIPCHK(hipStreamSynchronize(st[0]));
+	HIPCHK(hipStreamSynchronize(st[1]));
+fail:
+	for (int k = 0; k < 2; k++) {
+		if (st[k]) hipStreamSynchronize(st[k]);
+		hipHostFree(hbuf[k]);
+		hipHostFree(hl[k]);
+		hipFree(dbuf[k]);
+		hipFree(dl[k]);
+		hipFree(dv[k]);
+		if (done[k]) hipEventDestroy(done[k]);
+		if (st[k]) hipStreamDestroy(st[k]);
+	}
+	return err;
+}
+
+/* ------------------------------------------------------------------ stats */
+int xfg_stats_read_dev(xfg_ctx *ctx, int dev, struct xfg_stats_record out[XFG_ACTION_MAX])
+{
+	if (!ctx || !out || dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[dev];
+	unsigned long long s[10];
+	int err = dev_read(d, s, ctx->reduced ? d->red_stats : d->stats, sizeof(s));
+	if (err)
+		return err;
+	for (int a = 0; a < XFG_ACTION_MAX; a++) {
+		out[a].packets = s[2 * a];
+		out[a].bytes = s[2 * a + 1];
+	}
+	return 0;
+}
+
+int xfg_stats_read(xfg_ctx *ctx, struct xfg_stats_record out[XFG_ACTION_MAX])
+{
+	if (!ctx || !out)
+		return -EINVAL;
+	memset(out, 0, sizeof(*out) * XFG_ACTION_MAX);
+	if (ctx->reduced)   /* every rank holds the job-wide sum already */
+		return ctx->ndev ? xfg_stats_read_dev(ctx, 0, out) : 0;
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_stats_record r[XFG_ACTION_MAX];
+		int err = xfg_stats_read_dev(ctx, i, r);
+		if (err)
+			return err;
+		for (int a = 0; a < XFG_ACTION_MAX; a++) {
+			out[a].packets += r[a].packets;
+			out[a].bytes += r[a].bytes;
+		}
+	}
+	return 0;
+}
+
+int xfg_stats_reset(xfg_ctx *ctx)
+{
+	if (!ctx)
+		return -EINVAL;
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		unsigned long long z[10] = { 0 };
+		int err = dev_write(d, d->stats, z, sizeof(z));
+		if (err)
+			return err;
+	}
+	ctx->reduced = 0;
+	return 0;
+}
+
+int xfg_sync(xfg_ctx *ctx)
+{
+	if (!ctx)
+		return -EINVAL;
+	for (int i = 0; i < ctx->ndev; i++) {
+		int err = hip_err(hipSetDevice(ctx->dev[i].ordinal));
+		if (!err)
+			err = hip_err(hipDeviceSynchronize());
+		if (err)
+			return err;
+	}
+	return 0;
+}
+
+/* ------------------------------------------------------------------ memory */
+void *xfg_dev_alloc(xfg_ctx *ctx, int dev, size_t bytes)
+{
+	void *p = NULL;
+	if (!ctx || dev < 0 || dev >= ctx->ndev)
+		return NULL;
+	if (hipSetDevice(ctx->dev[dev].ordinal) != hipSuccess)
+		return NULL;
+	if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess)
+		return NULL;
+	return p;
+}
+
+void xfg_dev_free(xfg_ctx *ctx, int dev, void *p)
+{
+	if (!ctx || dev < 0 || dev >= ctx->ndev || !p)
+		return;
+	hipSetDevice(ctx->dev[dev].ordinal);
+	hipFree(p);
+}
+
+int xfg_memcpy_h2d(xfg_ctx *ctx, int dev, void *dst, const void *src, size_t bytes)
+{
+	if (!ctx || dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	int err = hip_err(hipSetDevice(ctx->dev[dev].ordinal));
+	return err ? err : hip_err(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+}
+
+int xfg_memcpy_d2h(xfg_ctx *ctx, int dev, void *dst, const void *src, size_t bytes)
+{
+	if (!ctx || dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	int err = hip_err(hipSetDevice(ctx->dev[dev].ordinal));
+	if (!err)
+		err = hip_err(hipDeviceSynchronize());
+	return err ? err : hip_err(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+}
+
+void *xfg_host_alloc_pinned(size_t bytes)
+{
+	void *p = NULL;
+	if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess)
+		return NULL;
+	return p;
+}
+
+void xfg_host_free_pinned(void *p)
+{
+	if (p)
+		hipHostFree(p);
+}
+
+/* ------------------------------------------------------------------ RCCL */
+int xfg_comm_unique_id(uint8_t id[XFG_COMM_ID_BYTES])
+{
+	ncclUniqueId u;
+	if (sizeof(u) != XFG_COMM_ID_BYTES)
+		return -EINVAL;
+	if (ncclGetUniqueId(&u) != ncclSuccess)
+		return -EIO;
+	memcpy(id, &u, sizeof(u));
+	return 0;
+}
+
+int xfg_comm_init(xfg_ctx *ctx, int nranks, int rank, const uint8_t id[XFG_COMM_ID_BYTES])
+{
+	int err = 0;
+	ncclUniqueId u;
+	if (!ctx || ctx->ndev != 1 || nranks < 1 || rank < 0 || rank >= nranks)
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[0];
+	memcpy(&u, id, sizeof(u));
+	HIPCHK(hipSetDevice(d->ordinal));
+	for (int i = 0; i < NMAPS_HASH; i++)
+		HIPCHK(hipMalloc((void **)&d->m[i].red_hits, ((size_t)ctx->t[i].nslots + 1) * 8));
+	HIPCHK(hipMalloc((void **)&d->red_port_hits, XFG_PORT_MAP_ENTRIES * 8));
+	HIPCHK(hipMalloc((void **)&d->red_stats, 10 * 8));
+	if (ncclCommInitRank(&ctx->comm, nranks, u, rank) != ncclSuccess)
+		return -EIO;
+	ctx->comm_ready = 1;
+	return 0;
+fail:
+	return err;
+}
+
+int xfg_comm_allreduce(xfg_ctx *ctx)
+{
+	int err = 0;
+	if (!ctx || !ctx->comm_ready)
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[0];
+	HIPCHK(hipSetDevice(d->ordinal));
+	HIPCHK(hipStreamSynchronize(d->stream));
+	if (ncclGroupStart() != ncclSuccess)
+		return -EIO;
+	for (int i = 0; i < NMAPS_HASH; i++)
+		ncclAllReduce(d->m[i].hits, d->m[i].red_hits, (size_t)ctx->t[i].nslots + 1,
+			      ncclUint64, ncclSum, ctx->comm, d->stream);
+	ncclAllReduce(d->port_hits, d->red_port_hits, XFG_PORT_MAP_ENTRIES, ncclUint64, ncclSum,
+		      ctx->comm, d->stream);
+	ncclAllReduce(d->stats, d->red_stats, 10, ncclUint64, ncclSum, ctx->comm, d->stream);
+	if (ncclGroupEnd() != ncclSuccess)
+		return -EIO;
+	HIPCHK(hipStreamSynchronize(d->stream));
+	ctx->reduced = 1;
+	return 0;
+fail:
+	return err;
+}

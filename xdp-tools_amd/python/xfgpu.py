@@ -1,0 +1,379 @@
+"""xfgpu — Python (ctypes) view of the xdp-filter GPU C ABI (include/xdpfilter_gpu.h).
+
+The product is the C library xdp-tools_amd/lib/libxdpfilter_gpu.so; this
+module is the thin binding the tests and bench.py drive it through.  It
+mirrors the reference's operations on its pinned maps
+(xdp-filter/xdp-filter.c:73-157): per-device values like per-CPU values,
+negative-errno errors raised as OSError.
+
+There is no fallback: if the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import os
+import sys
+
+# One HIP runtime per process: torch ships its own libamdhip64 with the same
+# SONAME; loading torch first makes this library bind to that copy instead of
+# loading a second runtime next to it.
+try:  # pragma: no cover - environment dependent
+    import torch  # noqa: F401
+except Exception:  # torch absent: the library uses /opt/rocm's runtime
+    pass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libxdpfilter_gpu.so")
+
+FEAT_TCP, FEAT_UDP, FEAT_IPV6, FEAT_IPV4, FEAT_ETHERNET = 1, 2, 4, 8, 16
+FEAT_ALL = 31
+FEAT_ALLOW, FEAT_DENY = 32, 64
+MAP_PORTS, MAP_IPV4, MAP_IPV6, MAP_ETHERNET = 0, 1, 2, 3
+KEYLEN = {MAP_PORTS: 4, MAP_IPV4: 4, MAP_IPV6: 16, MAP_ETHERNET: 6}
+ACTION_MAX = 5
+
+# Every symbol include/xdpfilter_gpu.h declares (checked by the CPU tests).
+EXPORTS = [
+    "xfg_select_program", "xfg_open", "xfg_close", "xfg_prog_name", "xfg_prog_features",
+    "xfg_num_devices", "xfg_strerror", "xfg_map_lookup", "xfg_map_update", "xfg_map_delete",
+    "xfg_map_get_next_key", "xfg_map_count", "xfg_map_update_batch", "xfg_map_lookup_batch", "xfg_classify",
+    "xfg_classify_host", "xfg_stats_read", "xfg_stats_read_dev", "xfg_stats_reset",
+    "xfg_sync", "xfg_dev_alloc", "xfg_dev_free", "xfg_memcpy_h2d", "xfg_memcpy_d2h",
+    "xfg_host_alloc_pinned", "xfg_host_free_pinned", "xfg_classify_timed", "xfg_stream_read_timed",
+    "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce",
+]
+
+
+class OpenOpts(C.Structure):
+    _fields_ = [("sz", C.c_size_t), ("features", C.c_uint32),
+                ("devices", C.POINTER(C.c_int)), ("ndev", C.c_int),
+                ("ipv4_capacity", C.c_uint32), ("ipv6_capacity", C.c_uint32),
+                ("eth_capacity", C.c_uint32), ("hash_seed", C.c_uint32)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("lens", C.c_void_p),
+                ("count", C.c_uint64), ("stride", C.c_uint32), ("lens_u16", C.c_uint32)]
+
+
+class StatsRecord(C.Structure):
+    _fields_ = [("packets", C.c_uint64), ("bytes", C.c_uint64)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built (run `make` at the repo root)")
+    lib = C.CDLL(LIB_PATH)
+    vp, u64p = C.c_void_p, C.POINTER(C.c_uint64)
+    sig = {
+        "xfg_select_program": (C.c_int, [C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32)]),
+        "xfg_open": (C.c_int, [C.POINTER(vp), C.POINTER(OpenOpts)]),
+        "xfg_close": (None, [vp]),
+        "xfg_prog_name": (C.c_char_p, [vp]),
+        "xfg_prog_features": (C.c_uint32, [vp]),
+        "xfg_num_devices": (C.c_int, [vp]),
+        "xfg_strerror": (C.c_char_p, [C.c_int]),
+        "xfg_map_lookup": (C.c_int, [vp, C.c_int, vp, u64p]),
+        "xfg_map_update": (C.c_int, [vp, C.c_int, vp, u64p]),
+        "xfg_map_delete": (C.c_int, [vp, C.c_int, vp]),
+        "xfg_map_get_next_key": (C.c_int, [vp, C.c_int, vp, vp]),
+        "xfg_map_count": (C.c_int64, [vp, C.c_int]),
+        "xfg_map_update_batch": (C.c_int, [vp, C.c_int, vp, u64p, C.c_uint64]),
+        "xfg_map_lookup_batch": (C.c_int64, [vp, C.c_int, vp, C.c_uint64, u64p,
+                                             C.POINTER(C.c_uint8)]),
+        "xfg_classify": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, vp]),
+        "xfg_classify_host": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp]),
+        "xfg_classify_timed": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, C.c_int,
+                                         C.POINTER(C.c_double)]),
+        "xfg_stream_read_timed": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_int,
+                                            C.POINTER(C.c_double)]),
+        "xfg_stats_read": (C.c_int, [vp, C.POINTER(StatsRecord)]),
+        "xfg_stats_read_dev": (C.c_int, [vp, C.c_int, C.POINTER(StatsRecord)]),
+        "xfg_stats_reset": (C.c_int, [vp]),
+        "xfg_sync": (C.c_int, [vp]),
+        "xfg_dev_alloc": (vp, [vp, C.c_int, C.c_size_t]),
+        "xfg_dev_free": (None, [vp, C.c_int, vp]),
+        "xfg_memcpy_h2d": (C.c_int, [vp, C.c_int, vp, vp, C.c_size_t]),
+        "xfg_memcpy_d2h": (C.c_int, [vp, C.c_int, vp, vp, C.c_size_t]),
+        "xfg_host_alloc_pinned": (vp, [C.c_size_t]),
+        "xfg_host_free_pinned": (None, [vp]),
+        "xfg_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+        "xfg_comm_init": (C.c_int, [vp, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
+        "xfg_comm_allreduce": (C.c_int, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _check(rc, what=""):
+    if rc < 0:
+        raise OSError(-rc, f"{what}: {lib.xfg_strerror(rc).decode()} ({rc})")
+    return rc
+
+
+def select_program(features: int):
+    name = C.c_char_p()
+    feats = C.c_uint32()
+    _check(lib.xfg_select_program(features, C.byref(name), C.byref(feats)), "select_program")
+    return name.value.decode(), feats.value
+
+
+def _key_buf(map_id, key) -> C.Array:
+    kl = KEYLEN[map_id]
+    if map_id == MAP_PORTS and isinstance(key, int):
+        return (C.c_uint8 * 4).from_buffer_copy(int(key).to_bytes(4, "little"))
+    b = bytes(key)
+    if len(b) != kl:
+        raise ValueError(f"key must be {kl} bytes")
+    return (C.c_uint8 * kl).from_buffer_copy(b)
+
+
+class DeviceBuffer:
+    """hipMalloc'ed device memory owned through the C ABI."""
+
+    def __init__(self, filt: "Filter", dev: int, nbytes: int):
+        self.filt, self.dev, self.nbytes = filt, dev, nbytes
+        self.ptr = lib.xfg_dev_alloc(filt.ctx, dev, nbytes)
+        if not self.ptr:
+            raise MemoryError(f"xfg_dev_alloc({nbytes}) failed")
+
+    def upload(self, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _check(lib.xfg_memcpy_h2d(self.filt.ctx, self.dev, self.ptr, arr.ctypes.data, arr.nbytes), "h2d")
+
+    def download(self, arr: np.ndarray):
+        assert arr.flags.c_contiguous and arr.nbytes <= self.nbytes
+        _check(lib.xfg_memcpy_d2h(self.filt.ctx, self.dev, arr.ctypes.data, self.ptr, arr.nbytes), "d2h")
+        return arr
+
+    def free(self):
+        if self.ptr:
+            lib.xfg_dev_free(self.filt.ctx, self.dev, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Filter:
+    """One xfg context: a selected xdpfilt_* program, its maps, and devices."""
+
+    def __init__(self, features=FEAT_ALL | FEAT_DENY, devices=None, ndev=None,
+                 ipv4_capacity=0, ipv6_capacity=0, eth_capacity=0, hash_seed=0):
+        opts = OpenOpts()
+        opts.sz = C.sizeof(OpenOpts)
+        opts.features = features
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*devices)
+            self._devs = arr
+            opts.devices = arr
+            opts.ndev = len(devices)
+        else:
+            opts.ndev = 1 if ndev is None else ndev
+        opts.ipv4_capacity = ipv4_capacity
+        opts.ipv6_capacity = ipv6_capacity
+        opts.eth_capacity = eth_capacity
+        opts.hash_seed = hash_seed
+        ctx = C.c_void_p()
+        _check(lib.xfg_open(C.byref(ctx), C.byref(opts)), "xfg_open")
+        self.ctx = ctx
+        self.ndev = lib.xfg_num_devices(ctx)
+        self.prog_name = lib.xfg_prog_name(ctx).decode()
+        self.prog_features = lib.xfg_prog_features(ctx)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            lib.xfg_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def nvals(self):
+        return max(self.ndev, 1)
+
+    # -- maps ----------------------------------------------------------------
+    def lookup(self, map_id, key):
+        vals = (C.c_uint64 * self.nvals)()
+        _check(lib.xfg_map_lookup(self.ctx, map_id, _key_buf(map_id, key), vals), "lookup")
+        return list(vals)
+
+    def update(self, map_id, key, vals):
+        if isinstance(vals, int):
+            vals = [vals] * self.nvals
+        arr = (C.c_uint64 * self.nvals)(*vals)
+        _check(lib.xfg_map_update(self.ctx, map_id, _key_buf(map_id, key), arr), "update")
+
+    def delete(self, map_id, key):
+        _check(lib.xfg_map_delete(self.ctx, map_id, _key_buf(map_id, key)), "delete")
+
+    def keys(self, map_id):
+        kl = KEYLEN[map_id]
+        out, prev = [], None
+        nxt = (C.c_uint8 * kl)()
+        while True:
+            rc = lib.xfg_map_get_next_key(self.ctx, map_id, prev, nxt)
+            if rc == -errno.ENOENT:
+                return out
+            _check(rc, "get_next_key")
+            out.append(bytes(nxt))
+            prev = (C.c_uint8 * kl).from_buffer_copy(bytes(nxt))
+
+    def count(self, map_id):
+        return _check(lib.xfg_map_count(self.ctx, map_id), "count")
+
+    def update_batch(self, map_id, keys: np.ndarray, vals: np.ndarray):
+        keys = np.ascontiguousarray(keys, np.uint8)
+        vals = np.ascontiguousarray(vals, np.uint64)
+        _check(lib.xfg_map_update_batch(self.ctx, map_id, keys.ctypes.data,
+                                        vals.ctypes.data_as(C.POINTER(C.c_uint64)), len(vals)),
+               "update_batch")
+
+    def load_rules(self, rules):
+        """Load a tools.xftools.RuleSet (ports + hash maps) on every device."""
+        r = rules.prepared()
+        nz = np.nonzero(r.ports)[0]
+        if len(nz):
+            self.update_batch(MAP_PORTS, nz.astype("<u4").view(np.uint8), r.ports[nz])
+        if len(r.v4_vals):
+            self.update_batch(MAP_IPV4, r.v4_keys, r.v4_vals)
+        if len(r.v6_vals):
+            self.update_batch(MAP_IPV6, r.v6_keys, r.v6_vals)
+        if len(r.eth_vals):
+            self.update_batch(MAP_ETHERNET, r.eth_keys, r.eth_vals)
+
+    def lookup_batch(self, map_id, keys: np.ndarray):
+        """Per-device values of many keys: (vals[n, ndev], present[n])."""
+        if map_id == MAP_PORTS:
+            keys = np.ascontiguousarray(np.asarray(keys, dtype="<u4")).view(np.uint8)
+        keys = np.ascontiguousarray(keys, np.uint8)
+        n = len(keys) // KEYLEN[map_id] if keys.ndim == 1 else len(keys)
+        vals = np.zeros((n, self.nvals), np.uint64)
+        present = np.zeros(n, np.uint8)
+        _check(lib.xfg_map_lookup_batch(self.ctx, map_id, keys.ctypes.data, n,
+                                        vals.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                        present.ctypes.data_as(C.POINTER(C.c_uint8))),
+               "lookup_batch")
+        return vals, present
+
+    def values_of(self, map_id, keys: np.ndarray, dev=None):
+        """Per-rule values in key order: one device's, or summed over devices
+        the way the CLI sums per-CPU counters (flags from the first device)."""
+        vals, _ = self.lookup_batch(map_id, keys)
+        if dev is not None:
+            return vals[:, dev].copy()
+        hits = (vals >> np.uint64(6)).sum(axis=1, dtype=np.uint64)
+        return (hits << np.uint64(6)) | (vals[:, 0] & np.uint64(63))
+
+    # -- data path -------------------------------------------------------------
+    def alloc(self, nbytes, dev=0) -> DeviceBuffer:
+        return DeviceBuffer(self, dev, nbytes)
+
+    def classify(self, data_ptr, lens_ptr, count, stride, verdicts_ptr, offsets_ptr=None,
+                 lens_u16=False, dev=0, stream=None):
+        b = Batch(data_ptr, offsets_ptr, lens_ptr, count, stride, int(lens_u16))
+        _check(lib.xfg_classify(self.ctx, dev, C.byref(b), verdicts_ptr, stream), "classify")
+
+    def classify_timed(self, data_ptr, lens_ptr, count, stride, verdicts_ptr, iters,
+                       offsets_ptr=None, lens_u16=False, dev=0):
+        b = Batch(data_ptr, offsets_ptr, lens_ptr, count, stride, int(lens_u16))
+        ms = C.c_double()
+        _check(lib.xfg_classify_timed(self.ctx, dev, C.byref(b), verdicts_ptr, iters,
+                                      C.byref(ms)), "classify_timed")
+        return ms.value
+
+    def stream_read_timed(self, ptr, nbytes, iters, dev=0):
+        ms = C.c_double()
+        _check(lib.xfg_stream_read_timed(self.ctx, dev, ptr, nbytes, iters, C.byref(ms)),
+               "stream_read_timed")
+        return ms.value
+
+    def classify_host(self, data: np.ndarray, lens: np.ndarray, stride=0, offsets=None, dev=0):
+        """Host-resident batch (copies included); returns verdicts."""
+        n = len(lens)
+        verdicts = np.zeros(n, np.uint8)
+        lens = np.ascontiguousarray(lens)
+        offs = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
+        b = Batch(data.ctypes.data, None if offs is None else offs.ctypes.data,
+                  lens.ctypes.data, n, stride, int(lens.dtype == np.uint16))
+        _check(lib.xfg_classify_host(self.ctx, dev, C.byref(b), verdicts.ctypes.data),
+               "classify_host")
+        return verdicts
+
+    def run(self, data: np.ndarray, lens: np.ndarray, stride=0, offsets=None, dev=0):
+        """Upload a host batch, classify it on the device, return verdicts
+        (test convenience: device-resident classify + explicit copies)."""
+        n = len(lens)
+        lens = np.ascontiguousarray(lens)
+        d_data = self.alloc(max(data.nbytes, 16) + 64, dev)
+        d_data.upload(data)
+        d_lens = self.alloc(max(lens.nbytes, 16), dev)
+        d_lens.upload(lens)
+        d_offs = None
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, np.uint64)
+            d_offs = self.alloc(max(offsets.nbytes, 16), dev)
+            d_offs.upload(offsets)
+        d_v = self.alloc(max(n, 16), dev)
+        self.classify(d_data.ptr, d_lens.ptr, n, stride, d_v.ptr,
+                      offsets_ptr=None if d_offs is None else d_offs.ptr,
+                      lens_u16=lens.dtype == np.uint16, dev=dev)
+        self.sync()
+        out = np.zeros(n, np.uint8)
+        if n:
+            d_v.download(out)
+        for b in (d_data, d_lens, d_offs, d_v):
+            if b is not None:
+                b.free()
+        return out
+
+    def stats(self, dev=None) -> np.ndarray:
+        recs = (StatsRecord * ACTION_MAX)()
+        if dev is None:
+            _check(lib.xfg_stats_read(self.ctx, recs), "stats_read")
+        else:
+            _check(lib.xfg_stats_read_dev(self.ctx, dev, recs), "stats_read_dev")
+        return np.array([[r.packets, r.bytes] for r in recs], np.uint64)
+
+    def stats_reset(self):
+        _check(lib.xfg_stats_reset(self.ctx), "stats_reset")
+
+    def sync(self):
+        _check(lib.xfg_sync(self.ctx), "sync")
+
+    # -- multi-process -----------------------------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        _check(lib.xfg_comm_unique_id(buf), "comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib.xfg_comm_init(self.ctx, nranks, rank, buf), "comm_init")
+
+    def comm_allreduce(self):
+        _check(lib.xfg_comm_allreduce(self.ctx), "comm_allreduce")
