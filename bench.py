@@ -56,31 +56,8 @@ def main():
     import xftools as X
     import xfgpu as G
 
-    n = 1 << args.log2_packets
-    stride = 64
-    # ---- rules: 1M IPv4 dst rules (seed 3) + 16 dst-port rules (tcp,udp)
-    v4 = X.rand_keys(3, int(args.rules * 1.02) + 16, 4)[:args.rules]
-    ports = (np.arange(16, dtype=np.uint16) * 1031 + 53).astype(np.uint16)
-    # ---- traffic: C3 mix, shard seeded by rank
-    t0 = time.time()
-    data, lens = X.gen_workload(3 + 1000 * rank, 3, n, stride, v4=v4, ports=ports,
-                                dst_permille=500, port_permille=250, bad_permille=10)
-    lens16 = lens.astype(np.uint16)
-    gen_s = time.time() - t0
-
-    f = G.Filter(G.FEAT_ALL | G.FEAT_DENY, devices=[local], ipv4_capacity=args.rules)
-    assert f.prog_name == "xdpfilt_dny_all"
-    f.update_batch(G.MAP_IPV4, v4, np.full(len(v4), 2, np.uint64))           # dst
-    pkeys = np.array([X.port_key(int(p)) for p in ports], "<u4").view(np.uint8)
-    f.update_batch(G.MAP_PORTS, pkeys, np.full(len(ports), 2 | 4 | 8, np.uint64))
-    d_data = f.alloc(data.nbytes)
-    d_data.upload(data)
-    d_lens = f.alloc(lens16.nbytes)
-    d_lens.upload(lens16)
-    d_verd = f.alloc(n)
-    del data
-
-    alg_bytes = int(np.minimum(lens.astype(np.int64), 128).sum() + n)   # min(len,128)+1
+    f, bufs, n, stride, lens, alg_bytes, v4, ports, gen_s = setup(args, rank, local)
+    d_data, d_lens, d_verd = bufs
 
     def barrier():
         if dist is not None:
@@ -178,6 +155,41 @@ def main():
     f.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def setup(args, rank, local):
+    """Rules (1M IPv4 dst + 16 dst-port rules), the rank's C3 shard resident
+    in HBM, and a dny_all context on device `local`."""
+    import numpy as np
+    import xftools as X
+    import xfgpu as G
+    n = 1 << args.log2_packets
+    stride = 64
+    # ---- rules: 1M IPv4 dst rules (seed 3) + 16 dst-port rules (tcp,udp)
+    v4 = X.rand_keys(3, int(args.rules * 1.02) + 16, 4)[:args.rules]
+    ports = (np.arange(16, dtype=np.uint16) * 1031 + 53).astype(np.uint16)
+    # ---- traffic: C3 mix, shard seeded by rank
+    t0 = time.time()
+    data, lens = X.gen_workload(3 + 1000 * rank, 3, n, stride, v4=v4, ports=ports,
+                                dst_permille=500, port_permille=250, bad_permille=10)
+    lens16 = lens.astype(np.uint16)
+    gen_s = time.time() - t0
+
+    f = G.Filter(G.FEAT_ALL | G.FEAT_DENY, devices=[local], ipv4_capacity=args.rules)
+    assert f.prog_name == "xdpfilt_dny_all"
+    f.update_batch(G.MAP_IPV4, v4, np.full(len(v4), 2, np.uint64))           # dst
+    pkeys = np.array([X.port_key(int(p)) for p in ports], "<u4").view(np.uint8)
+    f.update_batch(G.MAP_PORTS, pkeys, np.full(len(ports), 2 | 4 | 8, np.uint64))
+    d_data = f.alloc(data.nbytes)
+    d_data.upload(data)
+    d_lens = f.alloc(lens16.nbytes)
+    d_lens.upload(lens16)
+    d_verd = f.alloc(n)
+    del data
+    return f, (d_data, d_lens, d_verd), n, stride, lens, alg_bytes, v4, ports, gen_s
+
+    alg_bytes = int(np.minimum(lens.astype(np.int64), 128).sum() + n)   # min(len,128)+1
+
 
 
 def cpu_baseline(X, np, v4, ports, seconds):

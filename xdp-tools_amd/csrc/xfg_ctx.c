@@ -755,6 +755,17 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 	 * stride; everything else stages 128 bytes (every synthetic class and all
 	 * common headers parse within 78 bytes; longer chains read HBM). */
 	a->window = (!b->offsets && b->stride && b->stride <= 64) ? 64 : 128;
+	/* Diagnostics only: XFG_ABLATE=<mask> (1 = treat every table as empty,
+	 * 2 = drop counter atomics, 4 = stage windows only).  Results are wrong
+	 * under any non-zero mask; bench.py --ablation uses it to split time. */
+	const char *ab = getenv("XFG_ABLATE");
+	if (ab && *ab) {
+		a->ablate = (uint32_t)strtoul(ab, NULL, 0);
+		if (a->ablate & 1) {
+			a->t4.count = a->t6.count = a->te.count = 0;
+			a->port_count = 0;
+		}
+	}
 }
 
 static unsigned grid_for(const struct xfg_dev *d, uint64_t n)

@@ -431,9 +431,14 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 		if (gi < a.n) {
 			len = load_len(a, gi);
 			Pkt<W> p{ &win[tid * ROWDW], pkt_ptr(a, gi), len };
-			act = classify_one<FEAT, W>(a, p, hitp);
+			if (a.ablate & 4)
+				act = p.u8(0) & 1;
+			else
+				act = classify_one<FEAT, W>(a, p, hitp);
 			a.verdicts[gi] = (uint8_t)act;
 		}
+		if (a.ablate & 2)
+			hitp = nullptr;
 
 		// counter bump, aggregated over same-slot lanes of the wave
 #pragma unroll 1

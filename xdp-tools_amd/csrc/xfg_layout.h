@@ -71,6 +71,8 @@ struct xfg_kargs {
 	uint32_t stride;
 	uint32_t lens_u16;
 	uint8_t *verdicts;
+	uint32_t ablate;              /* diagnostics only (XFG_ABLATE env), 0 in production:
+				       * 2 = no counter atomics, 4 = stage only (no parse) */
 };
 
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
