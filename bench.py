@@ -186,9 +186,9 @@ def setup(args, rank, local):
     d_lens.upload(lens16)
     d_verd = f.alloc(n)
     del data
-    return f, (d_data, d_lens, d_verd), n, stride, lens, alg_bytes, v4, ports, gen_s
 
     alg_bytes = int(np.minimum(lens.astype(np.int64), 128).sum() + n)   # min(len,128)+1
+    return f, (d_data, d_lens, d_verd), n, stride, lens, alg_bytes, v4, ports, gen_s
 
 
 

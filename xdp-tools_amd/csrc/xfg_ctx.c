@@ -7,7 +7,7 @@
  *   program selection     find_prog_file()          xdp-filter/xdp-filter.c:48-60
  *   BPF map CRUD          bpf_map_*_elem() on pinned per-CPU maps
  *                         (xdp-filter/xdp-filter.c:73-157; lib/util/util.h:29-33)
- *   per-CPU value copies  one value per device (flags + hits arrays in HBM)
+ *   per-CPU value copies  one value per device (flag bytes + hits in HBM)
  *   stats readout         map_get_value_percpu_array  lib/util/stats.c:140-172
  *   prog_lock_acquire     a context mutex           lib/util/util.c:727-767
  */
@@ -33,11 +33,11 @@ int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sink, unsigned
 			   void *stream);
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
+#define PORT_BITS_WORDS (XFG_PORT_MAP_ENTRIES / 32)
 
 struct dev_map {           /* device arrays of one hash map */
-	void *keys;
-	uint8_t *meta;
-	uint8_t *flags;
+	uint8_t *buckets;      /* (nbuckets + 1) * 64 B: keys, per-device flags, meta */
+	unsigned long long *bloom;
 	unsigned long long *hits;
 	unsigned long long *red_hits; /* reduction copy (multi-process) */
 };
@@ -49,6 +49,7 @@ struct xfg_dev {
 	hipEvent_t ev0, ev1;
 	struct dev_map m[NMAPS_HASH];
 	uint8_t *port_flags;
+	uint32_t *port_bits;
 	unsigned long long *port_hits;
 	unsigned long long *red_port_hits;
 	unsigned long long *stats;      /* 10 */
@@ -66,7 +67,8 @@ struct xfg_ctx {
 	/* host-only context: value store for ndev == 0 */
 	uint64_t *host_vals[NMAPS_HASH];
 	uint64_t *host_port_vals;
-	uint8_t *port_flags_host;        /* flags of device 0 view (for port_count) */
+	uint8_t *port_flags_host;        /* OR over devices of the port flags */
+	uint32_t *port_bits_host;        /* bit set <=> port_flags_host != 0 */
 	uint32_t port_count;
 	/* multi-process reduction */
 	ncclComm_t comm;
@@ -149,13 +151,13 @@ static void dev_free(struct xfg_dev *d)
 	if (hipSetDevice(d->ordinal) != hipSuccess)
 		return;
 	for (int i = 0; i < NMAPS_HASH; i++) {
-		hipFree(d->m[i].keys);
-		hipFree(d->m[i].meta);
-		hipFree(d->m[i].flags);
+		hipFree(d->m[i].buckets);
+		hipFree(d->m[i].bloom);
 		hipFree(d->m[i].hits);
 		hipFree(d->m[i].red_hits);
 	}
 	hipFree(d->port_flags);
+	hipFree(d->port_bits);
 	hipFree(d->port_hits);
 	hipFree(d->red_port_hits);
 	hipFree(d->stats);
@@ -183,18 +185,18 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	for (int i = 0; i < NMAPS_HASH; i++) {
 		const struct xfg_table *t = &ctx->t[i];
 		size_t ns = (size_t)t->nslots + 1;
-		HIPCHK(hipMalloc(&d->m[i].keys, (size_t)t->nbuckets * XFG_BUCKET_BYTES));
-		HIPCHK(hipMalloc((void **)&d->m[i].meta, t->nbuckets));
-		HIPCHK(hipMalloc((void **)&d->m[i].flags, ns));
+		HIPCHK(hipMalloc((void **)&d->m[i].buckets, xfg_table_img_bytes(t)));
+		HIPCHK(hipMalloc((void **)&d->m[i].bloom, (size_t)t->bloom_words * 8));
 		HIPCHK(hipMalloc((void **)&d->m[i].hits, ns * 8));
-		HIPCHK(hipMemset(d->m[i].keys, 0, (size_t)t->nbuckets * XFG_BUCKET_BYTES));
-		HIPCHK(hipMemset(d->m[i].meta, 0, t->nbuckets));
-		HIPCHK(hipMemset(d->m[i].flags, 0, ns));
+		HIPCHK(hipMemset(d->m[i].buckets, 0, xfg_table_img_bytes(t)));
+		HIPCHK(hipMemset(d->m[i].bloom, 0, (size_t)t->bloom_words * 8));
 		HIPCHK(hipMemset(d->m[i].hits, 0, ns * 8));
 	}
 	HIPCHK(hipMalloc((void **)&d->port_flags, XFG_PORT_MAP_ENTRIES));
+	HIPCHK(hipMalloc((void **)&d->port_bits, PORT_BITS_WORDS * 4));
 	HIPCHK(hipMalloc((void **)&d->port_hits, XFG_PORT_MAP_ENTRIES * 8));
 	HIPCHK(hipMemset(d->port_flags, 0, XFG_PORT_MAP_ENTRIES));
+	HIPCHK(hipMemset(d->port_bits, 0, PORT_BITS_WORDS * 4));
 	HIPCHK(hipMemset(d->port_hits, 0, XFG_PORT_MAP_ENTRIES * 8));
 	HIPCHK(hipMalloc((void **)&d->stats, 10 * 8));
 	HIPCHK(hipMemset(d->stats, 0, 10 * 8));
@@ -230,7 +232,8 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 	    (err = xfg_table_init(&ctx->t[2], 6, cape, seed ^ 0xbb67ae85u)))
 		goto fail;
 	ctx->port_flags_host = calloc(XFG_PORT_MAP_ENTRIES, 1);
-	if (!ctx->port_flags_host) {
+	ctx->port_bits_host = calloc(PORT_BITS_WORDS, 4);
+	if (!ctx->port_flags_host || !ctx->port_bits_host) {
 		err = -ENOMEM;
 		goto fail;
 	}
@@ -292,6 +295,7 @@ void xfg_close(xfg_ctx *ctx)
 	}
 	free(ctx->host_port_vals);
 	free(ctx->port_flags_host);
+	free(ctx->port_bits_host);
 	pthread_mutex_destroy(&ctx->lock);
 	free(ctx);
 }
@@ -321,6 +325,11 @@ static int dev_write(struct xfg_dev *d, void *dst, const void *src, size_t n)
 	return err;
 }
 
+static unsigned long long *hits_view(xfg_ctx *ctx, struct xfg_dev *d, int mi)
+{
+	return ctx->reduced ? d->m[mi].red_hits : d->m[mi].hits;
+}
+
 /* Read the per-device values of @slot of hash map @mi (0..2). */
 static int slot_values(xfg_ctx *ctx, int mi, uint64_t slot, uint64_t *vals)
 {
@@ -328,13 +337,14 @@ static int slot_values(xfg_ctx *ctx, int mi, uint64_t slot, uint64_t *vals)
 		vals[0] = ctx->host_vals[mi][slot];
 		return 0;
 	}
+	const struct xfg_table *t = &ctx->t[mi];
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
 		uint8_t f;
 		unsigned long long h;
-		int err = dev_read(d, &f, d->m[mi].flags + slot, 1);
+		int err = dev_read(d, &f, d->m[mi].buckets + xfg_table_flag_off(t, slot), 1);
 		if (!err)
-			err = dev_read(d, &h, (ctx->reduced ? d->m[mi].red_hits : d->m[mi].hits) + slot, 8);
+			err = dev_read(d, &h, hits_view(ctx, d, mi) + slot, 8);
 		if (err)
 			return err;
 		vals[i] = (h << XFG_COUNTER_SHIFT) | f;
@@ -348,11 +358,12 @@ static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals)
 		ctx->host_vals[mi][slot] = vals[0];
 		return 0;
 	}
+	const struct xfg_table *t = &ctx->t[mi];
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
 		uint8_t f = vals[i] & 63;
 		unsigned long long h = vals[i] >> XFG_COUNTER_SHIFT;
-		int err = dev_write(d, d->m[mi].flags + slot, &f, 1);
+		int err = dev_write(d, d->m[mi].buckets + xfg_table_flag_off(t, slot), &f, 1);
 		if (!err)
 			err = dev_write(d, d->m[mi].hits + slot, &h, 8);
 		if (err)
@@ -361,14 +372,27 @@ static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals)
 	return 0;
 }
 
-/* Push the key image of bucket @b of map @mi to every device. */
-static int push_bucket(xfg_ctx *ctx, int mi, uint32_t b)
+/* Push the key bytes of @slot (host image) to every device. */
+static int push_key(xfg_ctx *ctx, int mi, uint64_t slot)
+{
+	const struct xfg_table *t = &ctx->t[mi];
+	uint64_t off = xfg_table_key_off(t, slot);
+	for (int i = 0; i < ctx->ndev; i++) {
+		int err = dev_write(&ctx->dev[i], ctx->dev[i].m[mi].buckets + off, t->img + off,
+				    t->slot_bytes);
+		if (err)
+			return err;
+	}
+	return 0;
+}
+
+static int push_bloom(xfg_ctx *ctx, int mi, int64_t word)
 {
 	const struct xfg_table *t = &ctx->t[mi];
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
-		int err = dev_write(d, (uint8_t *)d->m[mi].keys + (size_t)b * XFG_BUCKET_BYTES,
-				    t->keys + (size_t)b * XFG_BUCKET_BYTES, XFG_BUCKET_BYTES);
+		int err = word < 0 ? dev_write(d, d->m[mi].bloom, t->bloom, (size_t)t->bloom_words * 8)
+				   : dev_write(d, d->m[mi].bloom + word, t->bloom + word, 8);
 		if (err)
 			return err;
 	}
@@ -381,9 +405,10 @@ static void meta_changed(void *arg, uint32_t b)
 {
 	struct meta_push *mp = arg;
 	xfg_ctx *ctx = mp->ctx;
+	uint64_t off = (uint64_t)b * XFG_BUCKET_BYTES + XFG_META_OFF;
 	for (int i = 0; i < ctx->ndev && !mp->err; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
-		mp->err = dev_write(d, d->m[mp->mi].meta + b, ctx->t[mp->mi].meta + b, 1);
+		mp->err = dev_write(d, d->m[mp->mi].buckets + off, ctx->t[mp->mi].img + off, 4);
 	}
 }
 
@@ -393,13 +418,29 @@ static int port_key(const void *key, uint32_t *k)
 	return *k < XFG_PORT_MAP_ENTRIES ? 0 : -ENOENT;
 }
 
-static void port_flags_note(xfg_ctx *ctx, uint32_t k, uint8_t f)
+/* Track which ports have any flag on any device: port_count (the empty-map
+ * skip) and the 65536-bit bitmap the kernel stages in LDS. */
+static int port_flags_note(xfg_ctx *ctx, uint32_t k, uint8_t f)
 {
 	if (!ctx->port_flags_host[k] && f)
 		ctx->port_count++;
 	else if (ctx->port_flags_host[k] && !f)
 		ctx->port_count--;
 	ctx->port_flags_host[k] = f;
+	uint32_t w = k / 32, before = ctx->port_bits_host[w];
+	if (f)
+		ctx->port_bits_host[w] |= 1u << (k % 32);
+	else
+		ctx->port_bits_host[w] &= ~(1u << (k % 32));
+	if (before == ctx->port_bits_host[w])
+		return 0;
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		int err = dev_write(d, d->port_bits + w, ctx->port_bits_host + w, 4);
+		if (err)
+			return err;
+	}
+	return 0;
 }
 
 int xfg_map_lookup(xfg_ctx *ctx, int map, const void *key, uint64_t *vals)
@@ -419,7 +460,7 @@ int xfg_map_lookup(xfg_ctx *ctx, int map, const void *key, uint64_t *vals)
 		for (int i = 0; i < ctx->ndev && !err; i++) {
 			struct xfg_dev *d = &ctx->dev[i];
 			uint8_t f;
-			unsigned long long h;
+			unsigned long long h = 0;
 			err = dev_read(d, &f, d->port_flags + k, 1);
 			if (!err)
 				err = dev_read(d, &h, (ctx->reduced ? d->red_port_hits : d->port_hits) + k, 8);
@@ -439,6 +480,28 @@ out:
 	return err;
 }
 
+static int port_store(xfg_ctx *ctx, uint32_t k, const uint64_t *vals)
+{
+	int err = 0;
+	uint8_t any = 0;
+	if (!ctx->ndev) {
+		ctx->host_port_vals[k] = vals[0];
+		any = vals[0] & 63;
+	}
+	for (int i = 0; i < ctx->ndev && !err; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		uint8_t f = vals[i] & 63;
+		unsigned long long h = vals[i] >> XFG_COUNTER_SHIFT;
+		any |= f;
+		err = dev_write(d, d->port_flags + k, &f, 1);
+		if (!err)
+			err = dev_write(d, d->port_hits + k, &h, 8);
+	}
+	if (!err)
+		err = port_flags_note(ctx, k, any);
+	return err;
+}
+
 int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals)
 {
 	int err = 0;
@@ -448,30 +511,10 @@ int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals)
 	ctx->reduced = 0;
 	if (map == XFG_MAP_PORTS) {
 		uint32_t k;
-		if ((err = port_key(key, &k))) {
+		if (port_key(key, &k))
 			err = -E2BIG; /* array map: index out of range */
-			goto out;
-		}
-		if (!ctx->ndev) {
-			ctx->host_port_vals[k] = vals[0];
-			port_flags_note(ctx, k, vals[0] & 63);
-			goto out;
-		}
-		for (int i = 0; i < ctx->ndev && !err; i++) {
-			struct xfg_dev *d = &ctx->dev[i];
-			uint8_t f = vals[i] & 63;
-			unsigned long long h = vals[i] >> XFG_COUNTER_SHIFT;
-			err = dev_write(d, d->port_flags + k, &f, 1);
-			if (!err)
-				err = dev_write(d, d->port_hits + k, &h, 8);
-		}
-		/* a port is "present" for the skip test if any device has flags */
-		{
-			uint8_t any = 0;
-			for (int i = 0; i < ctx->ndev; i++)
-				any |= vals[i] & 63;
-			port_flags_note(ctx, k, any);
-		}
+		else
+			err = port_store(ctx, k, vals);
 		goto out;
 	}
 	int mi = map - 1;
@@ -479,15 +522,19 @@ int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals)
 	int64_t s = xfg_table_find(t, key);
 	if (s < 0) {
 		struct meta_push mp = { ctx, mi, 0 };
-		s = xfg_table_insert(t, key, ctx->ndev ? meta_changed : NULL, &mp);
+		int64_t bw = -1;
+		s = xfg_table_insert(t, key, ctx->ndev ? meta_changed : NULL, &mp, &bw);
 		if (s < 0) {
 			err = (int)s;
 			goto out;
 		}
 		if ((err = mp.err))
 			goto out;
-		if ((uint64_t)s != t->nslots && ctx->ndev)
-			err = push_bucket(ctx, mi, (uint32_t)(s / t->slots_per_bucket));
+		if (ctx->ndev && (uint64_t)s != t->nslots) {
+			err = push_key(ctx, mi, (uint64_t)s);
+			if (!err && bw >= 0)
+				err = push_bloom(ctx, mi, bw);
+		}
 		if (err)
 			goto out;
 	}
@@ -524,7 +571,12 @@ int xfg_map_delete(xfg_ctx *ctx, int map, const void *key)
 			free(z);
 	}
 	if (!err && (uint64_t)s != t->nslots && ctx->ndev)
-		err = push_bucket(ctx, mi, (uint32_t)(s / t->slots_per_bucket));
+		err = push_key(ctx, mi, (uint64_t)s);
+	if (!err && xfg_table_bloom_needs_rebuild(t)) {
+		xfg_table_bloom_rebuild(t);
+		if (ctx->ndev)
+			err = push_bloom(ctx, mi, -1);
+	}
 out:
 	pthread_mutex_unlock(&ctx->lock);
 	return err;
@@ -553,10 +605,8 @@ int xfg_map_get_next_key(xfg_ctx *ctx, int map, const void *key, void *next_key)
 	pthread_mutex_lock(&ctx->lock);
 	const struct xfg_table *t = &ctx->t[map - 1];
 	int64_t after = -1;
-	if (key) {
-		int64_t s = xfg_table_find(t, key);
-		after = s; /* BPF htab: a missing key restarts at the first key */
-	}
+	if (key)
+		after = xfg_table_find(t, key); /* BPF htab: a missing key restarts at the first */
 	int64_t s = xfg_table_next_slot(t, after);
 	if (s < 0)
 		err = -ENOENT;
@@ -583,13 +633,14 @@ int64_t xfg_map_lookup_batch(xfg_ctx *ctx, int map, const void *keys, uint64_t n
 	if (!ctx || (!keys && n) || (!vals && n) || kl < 0)
 		return -EINVAL;
 	int nd = ctx->ndev ? ctx->ndev : 1;
-	size_t ns = map == XFG_MAP_PORTS ? XFG_PORT_MAP_ENTRIES
-					 : (size_t)ctx->t[map - 1].nslots + 1;
+	const struct xfg_table *t = map == XFG_MAP_PORTS ? NULL : &ctx->t[map - 1];
+	size_t ns = t ? (size_t)t->nslots + 1 : XFG_PORT_MAP_ENTRIES;
+	size_t fbytes = t ? xfg_table_img_bytes(t) : XFG_PORT_MAP_ENTRIES;
 	uint8_t *flags = NULL;
 	unsigned long long *hits = NULL;
 	pthread_mutex_lock(&ctx->lock);
 	if (ctx->ndev) {
-		flags = malloc(ns * nd);
+		flags = malloc(fbytes * nd);
 		hits = malloc(ns * 8 * nd);
 		if (!flags || !hits) {
 			err = -ENOMEM;
@@ -597,11 +648,11 @@ int64_t xfg_map_lookup_batch(xfg_ctx *ctx, int map, const void *keys, uint64_t n
 		}
 		for (int i = 0; i < ctx->ndev && !err; i++) {
 			struct xfg_dev *d = &ctx->dev[i];
-			const uint8_t *fsrc = map == XFG_MAP_PORTS ? d->port_flags : d->m[map - 1].flags;
+			const void *fsrc = t ? (const void *)d->m[map - 1].buckets : (const void *)d->port_flags;
 			const unsigned long long *hsrc =
-				map == XFG_MAP_PORTS ? (ctx->reduced ? d->red_port_hits : d->port_hits)
-						     : (ctx->reduced ? d->m[map - 1].red_hits : d->m[map - 1].hits);
-			err = dev_read(d, flags + ns * i, fsrc, ns);
+				t ? hits_view(ctx, d, map - 1)
+				  : (ctx->reduced ? d->red_port_hits : d->port_hits);
+			err = dev_read(d, flags + fbytes * i, fsrc, fbytes);
 			if (!err)
 				err = dev_read(d, hits + ns * i, hsrc, ns * 8);
 		}
@@ -611,22 +662,24 @@ int64_t xfg_map_lookup_batch(xfg_ctx *ctx, int map, const void *keys, uint64_t n
 	for (uint64_t i = 0; i < n; i++) {
 		const uint8_t *k = (const uint8_t *)keys + (size_t)kl * i;
 		int64_t s;
-		if (map == XFG_MAP_PORTS) {
+		if (!t) {
 			uint32_t pk;
 			s = port_key(k, &pk) ? -1 : (int64_t)pk;
 		} else {
-			s = xfg_table_find(&ctx->t[map - 1], k);
+			s = xfg_table_find(t, k);
 		}
 		if (present)
 			present[i] = s >= 0;
 		for (int d = 0; d < nd; d++) {
 			uint64_t v = 0;
 			if (s >= 0) {
-				if (!ctx->ndev)
-					v = map == XFG_MAP_PORTS ? ctx->host_port_vals[s]
-								 : ctx->host_vals[map - 1][s];
-				else
-					v = (hits[ns * d + s] << XFG_COUNTER_SHIFT) | flags[ns * d + s];
+				if (!ctx->ndev) {
+					v = t ? ctx->host_vals[map - 1][s] : ctx->host_port_vals[s];
+				} else {
+					uint8_t f = t ? flags[fbytes * d + xfg_table_flag_off(t, s)]
+						      : flags[fbytes * d + s];
+					v = (hits[ns * d + s] << XFG_COUNTER_SHIFT) | f;
+				}
 			}
 			vals[i * nd + d] = v;
 		}
@@ -646,43 +699,44 @@ int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t
 	if (!ctx || (!keys && n) || (!vals && n) || kl < 0)
 		return -EINVAL;
 	if (map == XFG_MAP_PORTS) {
+		uint64_t v[64];
+		uint64_t *vv = ctx->ndev > 64 ? calloc(ctx->ndev, 8) : v;
+		if (!vv)
+			return -ENOMEM;
 		for (uint64_t i = 0; i < n && !err; i++) {
-			uint64_t v[64];
-			uint64_t *vv = ctx->ndev > 64 ? calloc(ctx->ndev, 8) : v;
-			if (!vv)
-				return -ENOMEM;
 			for (int d = 0; d < (ctx->ndev ? ctx->ndev : 1); d++)
 				vv[d] = vals[i];
 			err = xfg_map_update(ctx, map, (const uint8_t *)keys + 4 * i, vv);
-			if (vv != v)
-				free(vv);
 		}
+		if (vv != v)
+			free(vv);
 		return err;
 	}
 	pthread_mutex_lock(&ctx->lock);
 	ctx->reduced = 0;
 	int mi = map - 1;
 	struct xfg_table *t = &ctx->t[mi];
-	size_t ns = (size_t)t->nslots + 1;
-	uint8_t *flags = NULL;
+	size_t ns = (size_t)t->nslots + 1, ib = xfg_table_img_bytes(t);
+	uint8_t *img = NULL;           /* per-device bucket images */
 	unsigned long long *hits = NULL;
-	int nd = ctx->ndev ? ctx->ndev : 1;
+	int nd = ctx->ndev;
+	int fresh = t->count == 0;     /* nothing on the devices worth preserving */
 
-	if (ctx->ndev) {
-		flags = malloc(ns * nd);
+	if (nd) {
+		img = malloc(ib * nd);
 		hits = malloc(ns * 8 * nd);
-		if (!flags || !hits) {
+		if (!img || !hits) {
 			err = -ENOMEM;
 			goto out;
 		}
-		for (int i = 0; i < ctx->ndev && !err; i++) {
+		for (int i = 0; i < nd && !err; i++) {
 			struct xfg_dev *d = &ctx->dev[i];
-			if (t->count) {
-				err = dev_read(d, flags + ns * i, d->m[mi].flags, ns);
+			if (!fresh) {
+				err = dev_read(d, img + ib * i, d->m[mi].buckets, ib);
 				if (!err)
 					err = dev_read(d, hits + ns * i, d->m[mi].hits, ns * 8);
 			} else {
-				memset(flags + ns * i, 0, ns);
+				memset(img + ib * i, 0, ib);
 				memset(hits + ns * i, 0, ns * 8);
 			}
 		}
@@ -693,35 +747,40 @@ int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t
 		const uint8_t *k = (const uint8_t *)keys + (size_t)kl * i;
 		int64_t s = xfg_table_find(t, k);
 		if (s < 0)
-			s = xfg_table_insert(t, k, NULL, NULL);
+			s = xfg_table_insert(t, k, NULL, NULL, NULL);
 		if (s < 0) {
 			err = (int)s;
 			break;
 		}
-		if (ctx->ndev) {
+		if (nd) {
 			for (int d = 0; d < nd; d++) {
-				flags[ns * d + s] = vals[i] & 63;
+				img[ib * d + xfg_table_flag_off(t, s)] = vals[i] & 63;
 				hits[ns * d + s] = vals[i] >> XFG_COUNTER_SHIFT;
 			}
 		} else {
 			ctx->host_vals[mi][s] = vals[i];
 		}
 	}
-	/* upload full images (also on partial failure: keys inserted so far stay) */
-	for (int i = 0; i < ctx->ndev; i++) {
+	/* merge host keys + meta into each device image (flags stay per device)
+	 * and upload; also on partial failure: keys inserted so far stay */
+	for (int i = 0; i < nd; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
-		int e2 = dev_write(d, d->m[mi].keys, t->keys, (size_t)t->nbuckets * XFG_BUCKET_BYTES);
-		if (!e2)
-			e2 = dev_write(d, d->m[mi].meta, t->meta, t->nbuckets);
-		if (!e2)
-			e2 = dev_write(d, d->m[mi].flags, flags + ns * i, ns);
+		uint8_t *di = img + ib * i;
+		for (uint64_t b = 0; b <= t->nbuckets; b++) {
+			memcpy(di + b * XFG_BUCKET_BYTES, t->img + b * XFG_BUCKET_BYTES, XFG_KEY_AREA);
+			memcpy(di + b * XFG_BUCKET_BYTES + XFG_META_OFF,
+			       t->img + b * XFG_BUCKET_BYTES + XFG_META_OFF, 4);
+		}
+		int e2 = dev_write(d, d->m[mi].buckets, di, ib);
 		if (!e2)
 			e2 = dev_write(d, d->m[mi].hits, hits + ns * i, ns * 8);
+		if (!e2)
+			e2 = dev_write(d, d->m[mi].bloom, t->bloom, (size_t)t->bloom_words * 8);
 		if (e2 && !err)
 			err = e2;
 	}
 out:
-	free(flags);
+	free(img);
 	free(hits);
 	pthread_mutex_unlock(&ctx->lock);
 	return err;
@@ -735,12 +794,12 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 	struct xfg_tdesc *td[NMAPS_HASH] = { &a->t4, &a->t6, &a->te };
 	for (int i = 0; i < NMAPS_HASH; i++) {
 		xfg_table_desc(&ctx->t[i], td[i]);
-		td[i]->keys = d->m[i].keys;
-		td[i]->meta = d->m[i].meta;
-		td[i]->flags = d->m[i].flags;
+		td[i]->buckets = d->m[i].buckets;
+		td[i]->bloom = d->m[i].bloom;
 		td[i]->hits = d->m[i].hits;
 	}
 	a->port_flags = d->port_flags;
+	a->port_bits = d->port_bits;
 	a->port_hits = d->port_hits;
 	a->port_count = ctx->port_count;
 	a->stats = d->stats;
@@ -757,7 +816,7 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 	a->window = (!b->offsets && b->stride && b->stride <= 64) ? 64 : 128;
 	/* Diagnostics only: XFG_ABLATE=<mask> (1 = treat every table as empty,
 	 * 2 = drop counter atomics, 4 = stage windows only).  Results are wrong
-	 * under any non-zero mask; bench.py --ablation uses it to split time. */
+	 * under any non-zero mask; tools/ablate.py uses it to split time. */
 	const char *ab = getenv("XFG_ABLATE");
 	if (ab && *ab) {
 		a->ablate = (uint32_t)strtoul(ab, NULL, 0);

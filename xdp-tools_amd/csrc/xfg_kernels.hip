@@ -8,19 +8,25 @@
 // specialise xdp-filter/xdpfilt_prog.h (FEAT = the program's _features word,
 // xdpfilt_prog.h:313-315), and by the header window W staged in LDS.
 //
-// Per workgroup tile of 256 packets:
-//   1. stage: the first min(len, W) bytes of each packet are copied from HBM
-//      into LDS with coalesced 16-byte non-temporal loads (a wave reads 1 KiB
-//      contiguous per instruction for the fixed-stride layout), one LDS row of
-//      W+4 bytes per packet (odd dword stride: conflict-free lane-per-packet
-//      reads);
-//   2. parse + match: one lane per packet runs the reference control flow
-//      (xdpfilt_prog.h:214-310 over headers/xdp/parsing_helpers.h) reading
-//      header fields from its LDS row (bytes past W, only ever reached by
-//      long IPv6 extension chains, are read from HBM);
-//   3. rule lookups probe the device hash tables (xfg_layout.h) with 16-byte
-//      loads of one 64-byte bucket line;
-//   4. the first hit's counter is bumped after the wave re-converges, with
+// Per workgroup tile of 256 packets (one lane per packet):
+//   1. stage: the first W bytes of every packet of the NEXT tile are loaded
+//      with coalesced 16-byte non-temporal loads into registers while the
+//      current tile is processed (the fixed-stride layout needs no length
+//      before loading, so nothing serialises the stream), then written to
+//      one LDS row of W+4 bytes per packet (odd dword stride: conflict-free
+//      lane-per-packet reads);
+//   2. parse: the reference control flow (xdpfilt_prog.h:214-310 over
+//      headers/xdp/parsing_helpers.h) is split into its side-effect-free
+//      part — header walk, bounds checks, key extraction — done first, and
+//      the ordered lookups done after; a packet's lookups and its abort
+//      point keep the reference order (eth dst, eth src, ip dst, ip src /
+//      ARP / NDISC target, port dst, port src; an abort of a later header
+//      only counts if every earlier lookup missed);
+//   3. lookups: a Bloom word per key (L2-resident) rejects most misses; the
+//      bucket lines of all surviving keys of a stage are loaded together
+//      (one 64-byte line holds 12 IPv4 keys, their flag bytes and the
+//      overflow bit), then evaluated in reference order;
+//   4. the first hit's counter is bumped once the wave re-converges, with
 //      same-slot lanes aggregated into one atomic (hot rules);
 //   5. verdict bytes are stored coalesced; per-action {packets, bytes}
 //      (headers/xdp/xdp_stats_kern.h:29-48) are reduced per wave, per
@@ -88,138 +94,43 @@ struct Pkt {
 	}
 };
 
-// ---------------------------------------------------------------- table probes
-__device__ __forceinline__ uint32_t next_bucket(uint32_t b, uint32_t nb)
-{
-	return b + 1 == nb ? 0 : b + 1;
-}
+// ---------------------------------------------------------------- parse result
+// Stages of lookups in reference order; `abort_at` = the first stage that is
+// not reached because a header check failed (the packet is ABORTED iff every
+// lookup of the earlier stages missed), NST = no abort.
+enum Stage : uint32_t { ST_ETH = 0, ST_IP = 1, ST_ND = 2, ST_L4 = 3, NST = 4 };
 
-// filter_ipv4 lookup (BPF hash: exact match); returns slot or -1.
-__device__ __forceinline__ int64_t find_v4(const xfg_tdesc &t, uint32_t k)
-{
-	if (k == 0)
-		return t.zero_present ? (int64_t)t.nslots : -1;
-	uint32_t b = xfg_home(xfg_hash_v4(k, t.seed), t.nbuckets);
-	for (uint32_t d = 0; d <= t.max_disp; d++) {
-		const uint4 *bk = reinterpret_cast<const uint4 *>(
-			static_cast<const uint8_t *>(t.keys) + (uint64_t)b * XFG_BUCKET_BYTES);
-		const uint4 q0 = bk[0], q1 = bk[1], q2 = bk[2], q3 = bk[3];
-		const uint32_t m = (q0.x == k) | (q0.y == k) << 1 | (q0.z == k) << 2 | (q0.w == k) << 3 |
-				   (q1.x == k) << 4 | (q1.y == k) << 5 | (q1.z == k) << 6 | (q1.w == k) << 7 |
-				   (q2.x == k) << 8 | (q2.y == k) << 9 | (q2.z == k) << 10 | (q2.w == k) << 11 |
-				   (q3.x == k) << 12 | (q3.y == k) << 13 | (q3.z == k) << 14 | (q3.w == k) << 15;
-		if (m)
-			return (int64_t)b * XFG_SLOTS_V4 + (__builtin_ctz(m));
-		if (!(t.meta[b] & XFG_META_OVERFLOW))
-			return -1;
-		b = next_bucket(b, t.nbuckets);
-	}
-	return -1;
-}
+struct Parsed {
+	uint32_t abort_at;     // Stage
+	uint32_t l3;           // 0 none, 1 IPv4, 2 ARP, 3 IPv6
+	uint32_t arp_op;
+	uint32_t k4a, k4b;     // IPv4: dst, src | ARP: sip, tip
+	uint32_t o6;           // IPv6 header offset (saddr o6+8, daddr o6+24)
+	uint32_t nd;           // NDISC: 0 none, 135 NS, 136 NA
+	uint32_t ond;          // target offset
+	uint32_t l4proto;      // 17 / 6 when an L4 stage runs, else 0
+	uint32_t pdst, psrc;   // raw be16 port keys
+};
 
-// filter_ipv6 lookup: 16-byte keys, 4 per bucket.
-__device__ __forceinline__ int64_t find_v6(const xfg_tdesc &t, uint32_t w0, uint32_t w1,
-					   uint32_t w2, uint32_t w3)
-{
-	if ((w0 | w1 | w2 | w3) == 0)
-		return t.zero_present ? (int64_t)t.nslots : -1;
-	uint32_t b = xfg_home(xfg_hash_v6(w0, w1, w2, w3, t.seed), t.nbuckets);
-	for (uint32_t d = 0; d <= t.max_disp; d++) {
-		const uint4 *bk = reinterpret_cast<const uint4 *>(
-			static_cast<const uint8_t *>(t.keys) + (uint64_t)b * XFG_BUCKET_BYTES);
-		const uint4 q[4] = { bk[0], bk[1], bk[2], bk[3] };
-#pragma unroll
-		for (int i = 0; i < 4; i++)
-			if (q[i].x == w0 && q[i].y == w1 && q[i].z == w2 && q[i].w == w3)
-				return (int64_t)b * XFG_SLOTS_V6 + i;
-		if (!(t.meta[b] & XFG_META_OVERFLOW))
-			return -1;
-		b = next_bucket(b, t.nbuckets);
-	}
-	return -1;
-}
-
-// filter_ethernet lookup: MAC in the low 48 bits of a u64, 8 per bucket.
-__device__ __forceinline__ int64_t find_eth(const xfg_tdesc &t, uint64_t mac)
-{
-	if (mac == 0)
-		return t.zero_present ? (int64_t)t.nslots : -1;
-	uint32_t b = xfg_home(xfg_hash_eth(mac, t.seed), t.nbuckets);
-	for (uint32_t d = 0; d <= t.max_disp; d++) {
-		const uint64_t *bk = reinterpret_cast<const uint64_t *>(
-			static_cast<const uint8_t *>(t.keys) + (uint64_t)b * XFG_BUCKET_BYTES);
-		uint64_t q[8];
-#pragma unroll
-		for (int i = 0; i < 8; i++)
-			q[i] = bk[i];
-#pragma unroll
-		for (int i = 0; i < 8; i++)
-			if (q[i] == mac)
-				return (int64_t)b * XFG_SLOTS_ETH + i;
-		if (!(t.meta[b] & XFG_META_OVERFLOW))
-			return -1;
-		b = next_bucket(b, t.nbuckets);
-	}
-	return -1;
-}
-
-// CHECK_MAP (xdp-filter/xdpfilt_prog.h:56-64): hit iff the key exists and
-// (value & mask) == mask.  The counter bump is deferred to the caller.
-__device__ __forceinline__ bool check_slot(const xfg_tdesc &t, int64_t slot, uint32_t mask,
-					   unsigned long long *&hitp)
-{
-	if (slot >= 0 && (t.flags[slot] & mask) == mask) {
-		hitp = t.hits + slot;
-		return true;
-	}
-	return false;
-}
-
-__device__ __forceinline__ bool check_port(const xfg_kargs &a, uint32_t key, uint32_t mask,
-					   unsigned long long *&hitp)
-{
-	if ((a.port_flags[key] & mask) == mask) {
-		hitp = a.port_hits + key;
-		return true;
-	}
-	return false;
-}
-
-// lookup_verdict_ipv4 (xdpfilt_prog.h:121-134): dst first, then src.
-__device__ __forceinline__ bool v4_hit(const xfg_kargs &a, bool has_src, uint32_t src,
-				       bool has_dst, uint32_t dst, unsigned long long *&hitp)
-{
-	if (!a.t4.count)
-		return false;
-	if (has_dst && check_slot(a.t4, find_v4(a.t4, dst), M_DST, hitp))
-		return true;
-	if (has_src && check_slot(a.t4, find_v4(a.t4, src), M_SRC, hitp))
-		return true;
-	return false;
-}
-
-template <int W>
-__device__ __forceinline__ bool v6_check(const xfg_kargs &a, const Pkt<W> &p, uint32_t o,
-					 uint32_t mask, unsigned long long *&hitp)
-{
-	return check_slot(a.t6, find_v6(a.t6, p.u32(o), p.u32(o + 4), p.u32(o + 8), p.u32(o + 12)),
-			  mask, hitp);
-}
-
-// ---------------------------------------------------------------- the program
-// xdpfilt_prog.h:214-310 for one packet; returns the xdp action and sets
-// hitp to the counter of the first matching rule (or leaves it null).
 template <uint32_t FEAT, int W>
-__device__ uint32_t classify_one(const xfg_kargs &a, const Pkt<W> &p,
-				 unsigned long long *&hitp)
+__device__ __forceinline__ Parsed parse(const Pkt<W> &p)
 {
-	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;   // VERDICT_HIT
-	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;  // VERDICT_MISS
+	Parsed r;
+	r.abort_at = NST;
+	r.l3 = 0;
+	r.nd = 0;
+	r.l4proto = 0;
+	r.arp_op = 0;
+	r.k4a = r.k4b = 0;
+	r.o6 = r.ond = 0;
+	r.pdst = r.psrc = 0;
 	const uint32_t len = p.len;
 
 	// parse_ethhdr (parsing_helpers.h:100-134), VLAN_MAX_DEPTH 4
-	if (14 > len)
-		return A_ABORTED;
+	if (14 > len) {
+		r.abort_at = ST_ETH;
+		return r;
+	}
 	uint32_t proto = p.be16(12), off = 14;
 #pragma unroll
 	for (int i = 0; i < 4; i++) {
@@ -230,63 +141,51 @@ __device__ uint32_t classify_one(const xfg_kargs &a, const Pkt<W> &p,
 		proto = p.be16(off + 2);
 		off += 4;
 	}
-
-	// lookup_verdict_ethernet (xdpfilt_prog.h:187-196)
-	if constexpr ((FEAT & F_ETH) != 0) {
-		if (a.te.count) {
-			const uint64_t dmac = p.u32(0) | ((uint64_t)p.raw16(4) << 32);
-			if (check_slot(a.te, find_eth(a.te, dmac), M_DST, hitp))
-				return HIT;
-			const uint64_t smac = p.u32(6) | ((uint64_t)p.raw16(10) << 32);
-			if (check_slot(a.te, find_eth(a.te, smac), M_SRC, hitp))
-				return HIT;
-		}
-	}
-
 	if constexpr ((FEAT & (F_IPV4 | F_IPV6 | F_TCP | F_UDP)) == 0) {
-		return MISS;
+		return r;
 	} else {
 		uint32_t ip_type = 0, l4 = 0;
 		if (proto == 0x0800) {
 			// __parse_iphdr, frags_ok = 1 (parsing_helpers.h:201-227)
-			if (off + 20 > len)
-				return A_ABORTED;
+			if (off + 20 > len) {
+				r.abort_at = ST_IP;
+				return r;
+			}
 			const uint32_t hdrsize = (p.u8(off) & 0xF) * 4;
-			if (off + hdrsize > len)
-				return A_ABORTED;
+			if (off + hdrsize > len) {
+				r.abort_at = ST_IP;
+				return r;
+			}
 			ip_type = p.u8(off + 9);
 			l4 = off + hdrsize;
+			r.l3 = 1;
 			if constexpr ((FEAT & F_IPV4) != 0) {
-				if (v4_hit(a, true, p.u32(off + 12), true, p.u32(off + 16), hitp))
-					return HIT;
+				r.k4a = p.u32(off + 16);   // daddr: checked first
+				r.k4b = p.u32(off + 12);   // saddr
 			}
 		} else if ((FEAT & F_IPV4) && proto == 0x0806) {
 			// parse_arphdr (parsing_helpers.h:235-253), xdpfilt_prog.h:241-261
-			if (off + 28 > len)
-				return A_ABORTED;
-			if (p.be16(off) != 1 || p.be16(off + 2) != 0x0800 || p.u8(off + 4) != 6 ||
-			    p.u8(off + 5) != 4)
-				return A_ABORTED;
-			const uint32_t op = p.be16(off + 6);
-			const uint32_t sip = p.u32(off + 14), tip = p.u32(off + 24);
-			if (v4_hit(a, true, sip, false, 0, hitp))
-				return HIT;
-			if (op == 1) {          // ARPOP_REQUEST: target is a DST
-				if (v4_hit(a, false, 0, true, tip, hitp))
-					return HIT;
-			} else if (op == 2) {   // ARPOP_REPLY: target is a SRC
-				if (v4_hit(a, true, tip, false, 0, hitp))
-					return HIT;
+			if (off + 28 > len || p.be16(off) != 1 || p.be16(off + 2) != 0x0800 ||
+			    p.u8(off + 4) != 6 || p.u8(off + 5) != 4) {
+				r.abort_at = ST_IP;
+				return r;
 			}
+			r.l3 = 2;
+			r.arp_op = p.be16(off + 6);
+			r.k4a = p.u32(off + 14);   // sip
+			r.k4b = p.u32(off + 24);   // tip
+			return r;                  // ip_type stays 0: no L4 stage
 		} else if (proto == 0x86DD) {
 			// __parse_ip6hdr + skip_ip6hdrext (parsing_helpers.h:136-199)
-			if (off + 40 > len)
-				return A_ABORTED;
+			if (off + 40 > len) {
+				r.abort_at = ST_IP;
+				return r;
+			}
 			uint32_t nh = p.u8(off + 6), cur = off + 40;
 			bool done = false;
 			for (int i = 0; i < 6; i++) {   // IPV6_EXT_MAX_CHAIN
 				if (cur + 2 > len)
-					return A_ABORTED;
+					break;
 				if (nh == 0 || nh == 60 || nh == 43 || nh == 135) {
 					const uint32_t hl = p.u8(cur + 1);
 					nh = p.u8(cur);
@@ -303,67 +202,335 @@ __device__ uint32_t classify_one(const xfg_kargs &a, const Pkt<W> &p,
 					break;
 				}
 			}
-			if (!done)
-				return A_ABORTED;
+			if (!done) {
+				r.abort_at = ST_IP;
+				return r;
+			}
 			ip_type = nh;
 			l4 = cur;
-			if constexpr ((FEAT & F_IPV6) != 0) {
-				if (a.t6.count) {   // lookup_verdict_ipv6: dst, then src
-					if (v6_check(a, p, off + 24, M_DST, hitp) ||
-					    v6_check(a, p, off + 8, M_SRC, hitp))
-						return HIT;
-				}
-			}
+			r.l3 = 3;
+			r.o6 = off;
 			if (ip_type == 58) {
-				// parse_icmp6hdr + NDISC target (xdpfilt_prog.h:268-287)
-				if (cur + 8 > len)
-					return A_ABORTED;
-				const uint32_t t = p.u8(cur);
-				cur += 8;
-				if (t == 135 || t == 136) {
-					if (cur + 16 > len)
-						return A_ABORTED;
-					if constexpr ((FEAT & F_IPV6) != 0) {
-						if (a.t6.count &&
-						    v6_check(a, p, cur, t == 135 ? M_DST : M_SRC, hitp))
-							return HIT;
-					}
+				// parse_icmp6hdr + NDISC target (xdpfilt_prog.h:268-287):
+				// checked after the IPv6 address lookups
+				if (cur + 8 > len) {
+					r.abort_at = ST_ND;
+					return r;
 				}
+				const uint32_t t = p.u8(cur);
+				if (t == 135 || t == 136) {
+					if (cur + 24 > len) {
+						r.abort_at = ST_ND;
+						return r;
+					}
+					r.nd = t;
+					r.ond = cur + 8;
+				}
+				return r;
 			}
 		} else {
-			return MISS;
+			return r;   // not IP: MISS after the ethernet stage
 		}
 
-		if constexpr ((FEAT & F_UDP) != 0) {
-			if (ip_type == 17) {
-				// parse_udphdr (parsing_helpers.h:303-321)
-				if (l4 + 8 > len)
-					return A_ABORTED;
-				if (p.be16(l4 + 4) < 8)
-					return A_ABORTED;
-				// lookup_verdict_udp (xdpfilt_prog.h:92-101)
-				if (a.port_count &&
-				    (check_port(a, p.raw16(l4 + 2), M_DST | M_UDP, hitp) ||
-				     check_port(a, p.raw16(l4), M_SRC | M_UDP, hitp)))
-					return HIT;
+		if ((FEAT & F_UDP) && ip_type == 17) {
+			// parse_udphdr (parsing_helpers.h:303-321)
+			if (l4 + 8 > len || p.be16(l4 + 4) < 8) {
+				r.abort_at = ST_L4;
+				return r;
 			}
-		}
-		if constexpr ((FEAT & F_TCP) != 0) {
-			if (ip_type == 6) {
-				// parse_tcphdr (parsing_helpers.h:326-344)
-				if (l4 + 20 > len)
-					return A_ABORTED;
-				if (l4 + (p.u8(l4 + 12) >> 4) * 4 > len)
-					return A_ABORTED;
-				// lookup_verdict_tcp (xdpfilt_prog.h:76-85)
-				if (a.port_count &&
-				    (check_port(a, p.raw16(l4 + 2), M_DST | M_TCP, hitp) ||
-				     check_port(a, p.raw16(l4), M_SRC | M_TCP, hitp)))
-					return HIT;
+			r.l4proto = 17;
+		} else if ((FEAT & F_TCP) && ip_type == 6) {
+			// parse_tcphdr (parsing_helpers.h:326-344)
+			if (l4 + 20 > len || l4 + (p.u8(l4 + 12) >> 4) * 4 > len) {
+				r.abort_at = ST_L4;
+				return r;
 			}
+			r.l4proto = 6;
+		} else {
+			return r;
 		}
-		return MISS;
+		r.pdst = p.raw16(l4 + 2);
+		r.psrc = p.raw16(l4);
+		return r;
 	}
+}
+
+// ---------------------------------------------------------------- table probes
+__device__ __forceinline__ const uint8_t *bucket_ptr(const xfg_tdesc &t, uint32_t b)
+{
+	return static_cast<const uint8_t *>(t.buckets) + (uint64_t)b * XFG_BUCKET_BYTES;
+}
+
+__device__ __forceinline__ bool bloom_maybe(const xfg_tdesc &t, uint32_t h)
+{
+	const unsigned long long w = t.bloom[xfg_bloom_word(h, t.bloom_words)];
+	const unsigned long long m = xfg_bloom_mask(h);
+	return (w & m) == m;
+}
+
+// One 64-byte bucket line held in registers.
+struct Line {
+	u32x4 q0, q1, q2, q3;
+	__device__ __forceinline__ uint32_t w(int i) const   // dword i of the line
+	{
+		return i < 4 ? q0[i] : i < 8 ? q1[i - 4] : i < 12 ? q2[i - 8] : q3[i - 12];
+	}
+	__device__ __forceinline__ uint32_t flag(int slot) const   // flag byte of slot
+	{
+		const uint32_t fw = slot < 4 ? q3.x : slot < 8 ? q3.y : q3.z;
+		return (fw >> (8 * (slot & 3))) & 0xff;
+	}
+	__device__ __forceinline__ bool overflow() const { return q3.w & XFG_META_OVERFLOW; }
+};
+
+__device__ __forceinline__ Line load_line(const xfg_tdesc &t, uint32_t b)
+{
+	const u32x4 *p = reinterpret_cast<const u32x4 *>(bucket_ptr(t, b));
+	Line l;
+	l.q0 = p[0];
+	l.q1 = p[1];
+	l.q2 = p[2];
+	l.q3 = p[3];
+	return l;
+}
+
+// Match result: slot (-1 = absent) and its flag byte.
+struct Hit {
+	int64_t slot;
+	uint32_t flags;
+};
+
+__device__ __forceinline__ int match_v4(const Line &l, uint32_t k)
+{
+	uint32_t m = 0;
+#pragma unroll
+	for (int i = 0; i < 12; i++)
+		m |= (uint32_t)(l.w(i) == k) << i;
+	return m ? __builtin_ctz(m) : -1;
+}
+
+__device__ __forceinline__ int match_v6(const Line &l, uint32_t w0, uint32_t w1, uint32_t w2,
+					uint32_t w3)
+{
+#pragma unroll
+	for (int i = 0; i < 3; i++)
+		if (l.w(4 * i) == w0 && l.w(4 * i + 1) == w1 && l.w(4 * i + 2) == w2 &&
+		    l.w(4 * i + 3) == w3)
+			return i;
+	return -1;
+}
+
+__device__ __forceinline__ int match_eth(const Line &l, uint32_t lo, uint32_t hi)
+{
+#pragma unroll
+	for (int i = 0; i < 6; i++)
+		if (l.w(2 * i) == lo && l.w(2 * i + 1) == hi)
+			return i;
+	return -1;
+}
+
+template <int KIND>
+__device__ __forceinline__ int match(const Line &l, uint32_t k0, uint32_t k1, uint32_t k2,
+				     uint32_t k3)
+{
+	if constexpr (KIND == 4)
+		return match_v4(l, k0);
+	else if constexpr (KIND == 6)
+		return match_v6(l, k0, k1, k2, k3);
+	else
+		return match_eth(l, k0, k1);
+}
+
+template <int KIND>
+constexpr uint32_t slots_of()
+{
+	return KIND == 4 ? XFG_SLOTS_V4 : KIND == 6 ? XFG_SLOTS_V6 : XFG_SLOTS_ETH;
+}
+
+// The zero key lives in bucket nbuckets, slot 0.
+__device__ __forceinline__ Hit zero_hit(const xfg_tdesc &t)
+{
+	if (!t.zero_present)
+		return { -1, 0 };
+	return { (int64_t)t.nslots, bucket_ptr(t, t.nbuckets)[XFG_FLAGS_OFF] };
+}
+
+// Continue a probe past a full home bucket (rare): linear over buckets.
+template <int KIND>
+__device__ __forceinline__ Hit probe_chain(const xfg_tdesc &t, uint32_t b, uint32_t k0, uint32_t k1,
+					uint32_t k2, uint32_t k3)
+{
+	for (uint32_t d = 1; d <= t.max_disp; d++) {
+		b = b + 1 == t.nbuckets ? 0 : b + 1;
+		const Line l = load_line(t, b);
+		const int i = match<KIND>(l, k0, k1, k2, k3);
+		if (i >= 0)
+			return { (int64_t)b * slots_of<KIND>() + i, l.flag(i) };
+		if (!l.overflow())
+			break;
+	}
+	return { -1, 0 };
+}
+
+// A pending lookup: hash computed, Bloom word tested, bucket line loaded.
+template <int KIND>
+struct Probe {
+	uint32_t k0, k1, k2, k3;
+	uint32_t b;
+	bool zero, live;
+	Line l;
+
+	__device__ __forceinline__ void start(const xfg_tdesc &t, bool want, uint32_t a0,
+					      uint32_t a1 = 0, uint32_t a2 = 0, uint32_t a3 = 0)
+	{
+		k0 = a0; k1 = a1; k2 = a2; k3 = a3;
+		zero = (a0 | a1 | a2 | a3) == 0;
+		live = false;
+		b = 0;
+		if (!want || zero)
+			return;
+		uint32_t h;
+		if constexpr (KIND == 4)
+			h = xfg_hash_v4(a0, t.seed);
+		else if constexpr (KIND == 6)
+			h = xfg_hash_v6(a0, a1, a2, a3, t.seed);
+		else
+			h = xfg_hash_eth(a0 | ((uint64_t)a1 << 32), t.seed);
+		b = xfg_home(h, t.nbuckets);
+		live = bloom_maybe(t, h);
+	}
+	__device__ __forceinline__ void fetch(const xfg_tdesc &t)
+	{
+		if (live)
+			l = load_line(t, b);
+	}
+	__device__ __forceinline__ Hit result(const xfg_tdesc &t, bool want) const
+	{
+		if (!want)
+			return { -1, 0 };
+		if (zero)
+			return zero_hit(t);
+		if (!live)
+			return { -1, 0 };
+		const int i = match<KIND>(l, k0, k1, k2, k3);
+		if (i >= 0)
+			return { (int64_t)b * slots_of<KIND>() + i, l.flag(i) };
+		if (l.overflow() && t.max_disp)
+			return probe_chain<KIND>(t, b, k0, k1, k2, k3);
+		return { -1, 0 };
+	}
+};
+
+// CHECK_MAP (xdp-filter/xdpfilt_prog.h:56-64): hit iff the key exists and
+// (value & mask) == mask; the counter bump is deferred to the caller.
+__device__ __forceinline__ bool take(const xfg_tdesc &t, const Hit &h, uint32_t mask,
+				     unsigned long long *&hitp)
+{
+	if (h.slot >= 0 && (h.flags & mask) == mask) {
+		hitp = t.hits + h.slot;
+		return true;
+	}
+	return false;
+}
+
+__device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s_pbits,
+					   uint32_t key, uint32_t mask, unsigned long long *&hitp)
+{
+	if (!((s_pbits[key >> 5] >> (key & 31)) & 1))
+		return false;
+	if ((a.port_flags[key] & mask) == mask) {
+		hitp = a.port_hits + key;
+		return true;
+	}
+	return false;
+}
+
+// ---------------------------------------------------------------- the program
+// Ordered lookups over a parsed packet; returns the xdp action and sets hitp
+// to the first matching rule's counter.
+template <uint32_t FEAT, int W>
+__device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p, const Parsed &r,
+					    const uint32_t *s_pbits, unsigned long long *&hitp)
+{
+	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;   // VERDICT_HIT
+	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;  // VERDICT_MISS
+
+	if (r.abort_at == ST_ETH)
+		return A_ABORTED;
+
+	// lookup_verdict_ethernet (xdpfilt_prog.h:187-196): dst then src
+	if constexpr ((FEAT & F_ETH) != 0) {
+		if (a.te.count) {
+			Probe<2> d, s;
+			d.start(a.te, true, p.u32(0), p.raw16(4));
+			s.start(a.te, true, p.u32(6), p.raw16(10));
+			d.fetch(a.te);
+			s.fetch(a.te);
+			if (take(a.te, d.result(a.te, true), M_DST, hitp) ||
+			    take(a.te, s.result(a.te, true), M_SRC, hitp))
+				return HIT;
+		}
+	}
+	if (r.abort_at == ST_IP)
+		return A_ABORTED;
+
+	if constexpr ((FEAT & F_IPV4) != 0) {
+		if (a.t4.count && (r.l3 == 1 || r.l3 == 2)) {
+			// IPv4: dst (k4a, DST) then src (k4b, SRC)  (xdpfilt_prog.h:121-134)
+			// ARP:  sip (k4a, SRC); op 1: tip DST; op 2: tip SRC  (:241-261)
+			const bool arp = r.l3 == 2;
+			const bool want_b = !arp || r.arp_op == 1 || r.arp_op == 2;
+			Probe<4> x, y;
+			x.start(a.t4, true, r.k4a);
+			y.start(a.t4, want_b, r.k4b);
+			x.fetch(a.t4);
+			y.fetch(a.t4);
+			const uint32_t mx = arp ? M_SRC : M_DST;
+			const uint32_t my = arp ? (r.arp_op == 1 ? M_DST : M_SRC) : M_SRC;
+			if (take(a.t4, x.result(a.t4, true), mx, hitp) ||
+			    take(a.t4, y.result(a.t4, want_b), my, hitp))
+				return HIT;
+		}
+	}
+	if constexpr ((FEAT & F_IPV6) != 0) {
+		if (a.t6.count && r.l3 == 3) {
+			// lookup_verdict_ipv6: dst then src (xdpfilt_prog.h:152-165)
+			const uint32_t o = r.o6;
+			Probe<6> d, s;
+			d.start(a.t6, true, p.u32(o + 24), p.u32(o + 28), p.u32(o + 32), p.u32(o + 36));
+			s.start(a.t6, true, p.u32(o + 8), p.u32(o + 12), p.u32(o + 16), p.u32(o + 20));
+			d.fetch(a.t6);
+			s.fetch(a.t6);
+			if (take(a.t6, d.result(a.t6, true), M_DST, hitp) ||
+			    take(a.t6, s.result(a.t6, true), M_SRC, hitp))
+				return HIT;
+		}
+	}
+	if (r.abort_at == ST_ND)
+		return A_ABORTED;
+	if constexpr ((FEAT & F_IPV6) != 0) {
+		if (a.t6.count && r.nd) {
+			// NDISC target: NS => DST, NA => SRC (xdpfilt_prog.h:277-285)
+			const uint32_t o = r.ond;
+			Probe<6> t;
+			t.start(a.t6, true, p.u32(o), p.u32(o + 4), p.u32(o + 8), p.u32(o + 12));
+			t.fetch(a.t6);
+			if (take(a.t6, t.result(a.t6, true), r.nd == 135 ? M_DST : M_SRC, hitp))
+				return HIT;
+		}
+	}
+	if (r.abort_at == ST_L4)
+		return A_ABORTED;
+	if constexpr ((FEAT & (F_UDP | F_TCP)) != 0) {
+		if (a.port_count && r.l4proto) {
+			// lookup_verdict_udp / _tcp (xdpfilt_prog.h:92-101 / :76-85)
+			const uint32_t pm = r.l4proto == 17 ? M_UDP : M_TCP;
+			if (check_port(a, s_pbits, r.pdst, M_DST | pm, hitp) ||
+			    check_port(a, s_pbits, r.psrc, M_SRC | pm, hitp))
+				return HIT;
+		}
+	}
+	return MISS;
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -391,50 +558,75 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 {
 	constexpr int CPP = W / 16;            // 16-byte chunks per packet window
 	constexpr int ROWDW = Pkt<W>::ROWDW;   // odd dword stride per LDS row
+	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	__shared__ uint32_t win[TILE * ROWDW];
+	__shared__ uint32_t s_pbits[PORTS ? 2048 : 1];
 	__shared__ unsigned long long s_stats[6];
 
 	const int tid = threadIdx.x;
 	const int lane = tid & 63;
 	if (tid < 6)
 		s_stats[tid] = 0;
+	if constexpr (PORTS) {
+		if (a.port_count)
+			for (int i = tid; i < 2048; i += TILE)
+				s_pbits[i] = a.port_bits[i];
+	}
+	// fixed-stride layout with stride >= W: every window byte is readable,
+	// so loads need no length (no load->load dependency on the stream)
+	const bool guarded = a.offsets != nullptr || a.stride < (uint32_t)W;
 
 	const uint64_t ntiles = (a.n + TILE - 1) / TILE;
-	for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-		const uint64_t base = tile * TILE;
-
-		// 1. stage header windows into LDS
+	uint64_t tile = blockIdx.x;
+	u32x4 pre[CPP];
+	uint32_t plen = 0;
+	auto issue = [&](uint64_t t) {
+		const uint64_t base = t * TILE;
 #pragma unroll
 		for (int it = 0; it < CPP; it++) {
 			const int c = it * TILE + tid;
 			const int pk = c / CPP, sub = c % CPP;
 			const uint64_t gi = base + pk;
-			if (gi < a.n) {
-				const uint32_t len = load_len(a, gi);
-				if ((uint32_t)sub * 16 < len) {
-					const u32x4 *src = reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16);
-					const u32x4 v = __builtin_nontemporal_load(src);
-					uint32_t *dst = &win[pk * ROWDW + sub * 4];
-					dst[0] = v.x;
-					dst[1] = v.y;
-					dst[2] = v.z;
-					dst[3] = v.w;
-				}
-			}
+			pre[it] = u32x4{ 0, 0, 0, 0 };
+			if (gi < a.n && (!guarded || (uint32_t)sub * 16 < load_len(a, gi)))
+				pre[it] = __builtin_nontemporal_load(
+					reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16));
 		}
+		plen = base + tid < a.n ? load_len(a, base + tid) : 0;
+	};
+	if (tile < ntiles)
+		issue(tile);
+
+	for (; tile < ntiles; tile += gridDim.x) {
+		const uint64_t base = tile * TILE;
+		// 1. stage the prefetched windows into LDS
+#pragma unroll
+		for (int it = 0; it < CPP; it++) {
+			const int c = it * TILE + tid;
+			const int pk = c / CPP, sub = c % CPP;
+			uint32_t *dst = &win[pk * ROWDW + sub * 4];
+			dst[0] = pre[it].x;
+			dst[1] = pre[it].y;
+			dst[2] = pre[it].z;
+			dst[3] = pre[it].w;
+		}
+		const uint32_t len = plen;
 		__syncthreads();
+		if (tile + gridDim.x < ntiles)
+			issue(tile + gridDim.x);   // next tile's stream overlaps this tile's work
 
 		// 2-4. parse, match, verdict
 		const uint64_t gi = base + tid;
-		uint32_t act = A_NONE, len = 0;
+		uint32_t act = A_NONE;
 		unsigned long long *hitp = nullptr;
 		if (gi < a.n) {
-			len = load_len(a, gi);
 			Pkt<W> p{ &win[tid * ROWDW], pkt_ptr(a, gi), len };
-			if (a.ablate & 4)
+			if (a.ablate & 4) {
 				act = p.u8(0) & 1;
-			else
-				act = classify_one<FEAT, W>(a, p, hitp);
+			} else {
+				const Parsed r = parse<FEAT, W>(p);
+				act = lookups<FEAT, W>(a, p, r, s_pbits, hitp);
+			}
 			a.verdicts[gi] = (uint8_t)act;
 		}
 		if (a.ablate & 2)
@@ -442,7 +634,7 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 
 		// counter bump, aggregated over same-slot lanes of the wave
 #pragma unroll 1
-		for (int r = 0; r < 4; r++) {
+		for (int rnd = 0; rnd < 4; rnd++) {
 			const unsigned long long pend = __ballot(hitp != nullptr);
 			if (!pend)
 				break;

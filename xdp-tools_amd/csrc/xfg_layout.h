@@ -4,62 +4,82 @@
  * and the HIP kernels.  Nothing here is part of the public C ABI.
  *
  * The reference's BPF_MAP_TYPE_PERCPU_HASH maps (filter_ipv4/ipv6/ethernet,
- * xdp-filter/xdpfilt_prog.h:113-185) become bucketed open-addressed tables:
+ * xdp-filter/xdpfilt_prog.h:113-185) become bucketed open-addressed tables,
+ * one 64-byte line per bucket so that ONE random read answers a probe:
  *
- *   keys  [nbuckets][64 B]  one 64-byte line per bucket:
- *                             ipv4: 16 x u32, ipv6: 4 x 16 B, ethernet: 8 x u64
- *                             (MAC in the low 48 bits, little-endian byte copy)
- *                           an all-zero key marks an empty slot; the all-zero
- *                           KEY itself lives in the extra slot `nslots`.
- *   meta  [nbuckets] u8     bit0 = overflow: some key whose probe sequence
- *                           passed this bucket was placed further on.
- *   flags [nslots+1] u8     low 6 bits of the reference value (MAP_FLAGS..)
- *   hits  [nslots+1] u64    reference value >> COUNTER_SHIFT
+ *   bytes  0..47  keys   ipv4: 12 x u32 | ipv6: 3 x 16 B | ethernet: 6 x u64
+ *                        (MAC in the low 48 bits, little-endian byte copy)
+ *   bytes 48..59  flags  one byte per slot: low 6 bits of the reference
+ *                        value (MAP_FLAG_* and the two spare bits)
+ *   bytes 60..63  meta   bit0 = overflow: a key whose probe sequence passed
+ *                        this bucket was placed further on
+ *
+ * An all-zero key marks an empty slot; the all-zero KEY itself lives in the
+ * extra bucket `nbuckets` (slot nslots = nbuckets * slots_per_bucket), which
+ * hashing never reaches.  Key bytes are identical on every device (slot
+ * indices agree across devices); flag bytes are per device, like the
+ * reference's per-CPU values.
+ *
+ *   hits  [nslots+1] u64   reference value >> COUNTER_SHIFT, per device
  *
  * so the reference value is exactly (hits << 6) | flags, and a hit's
  * `*value += 1 << COUNTER_SHIFT` (xdp-filter/xdpfilt_prog.h:60-61) becomes
  * hits += 1.  Keeping hits apart from flags lets the multi-GPU reduction sum
  * counters directly (ncclUint64) without disturbing the flag bits.
  *
- * Probing: home bucket h(key) (multiplicative range reduction of a 32-bit
- * murmur3 finaliser chain), then linear over buckets; lookup stops at a
- * bucket whose overflow bit is clear or after max_disp+1 buckets.  Keys never
- * move once placed, so slot indices (and hence per-device counters) are
- * stable across inserts and deletes.
+ * Probing: home bucket from a 32-bit murmur3-finaliser chain (multiplicative
+ * range reduction), then linear over buckets; a lookup stops at a bucket
+ * whose overflow bit is clear or after max_disp+1 buckets.  Keys never move
+ * once placed, so slot indices (and the per-device counters) are stable
+ * across inserts and deletes.
+ *
+ * Prefilter: a blocked Bloom filter of 64-bit words (one word per key, 4
+ * bits from a second hash) answers most negative lookups from a table small
+ * enough to stay in each XCD's L2.  Deleted keys leave their bits set
+ * (false positives only; the bucket probe decides), and the host rebuilds
+ * the filter when stale bits accumulate.
  *
  * filter_ports (PERCPU_ARRAY[65536], :67-73) is dense: flags[65536] u8 and
- * hits[65536] u64 indexed by the raw big-endian port value.
+ * hits[65536] u64 indexed by the raw big-endian port value, plus a 65536-bit
+ * "any flag set" bitmap that each workgroup stages in LDS.
  */
 #ifndef XFG_LAYOUT_H
 #define XFG_LAYOUT_H
 
 #include <stdint.h>
 
-#define XFG_BUCKET_BYTES 64u
-#define XFG_SLOTS_V4     16u
-#define XFG_SLOTS_V6     4u
-#define XFG_SLOTS_ETH    8u
+#define XFG_BUCKET_BYTES  64u
+#define XFG_KEY_AREA      48u
+#define XFG_FLAGS_OFF     48u
+#define XFG_META_OFF      60u
+#define XFG_SLOTS_V4      12u
+#define XFG_SLOTS_V6      3u
+#define XFG_SLOTS_ETH     6u
 
 #define XFG_META_OVERFLOW 1u
 
+#define XFG_BLOOM_K       4u
+
 /* Per-hash-map descriptor passed to the kernel by value. */
 struct xfg_tdesc {
-	const void *keys;
-	const uint8_t *meta;
-	const uint8_t *flags;
-	unsigned long long *hits;
+	const void *buckets;         /* (nbuckets + 1) * 64 B */
+	const unsigned long long *bloom; /* bloom_words x u64 */
+	unsigned long long *hits;    /* nslots + 1 */
 	uint32_t nbuckets;
 	uint32_t max_disp;
-	uint32_t count;        /* keys present; 0 => lookups can never hit */
-	uint32_t zero_present; /* the all-zero key is present (slot nslots) */
+	uint32_t count;              /* keys present; 0 => lookups can never hit */
+	uint32_t zero_present;       /* the all-zero key is present (slot nslots) */
 	uint32_t nslots;
 	uint32_t seed;
+	uint32_t bloom_words;        /* 0 => no prefilter */
+	uint32_t pad;
 };
 
 /* Kernel arguments of one classify launch. */
 struct xfg_kargs {
 	struct xfg_tdesc t4, t6, te;
 	const uint8_t *port_flags;
+	const uint32_t *port_bits;    /* 65536-bit "flags != 0" bitmap */
 	unsigned long long *port_hits;
 	uint32_t port_count;          /* ports with non-zero flags; 0 => skip */
 	uint32_t window;              /* header window staged in LDS (64 or 128) */
@@ -73,6 +93,7 @@ struct xfg_kargs {
 	uint8_t *verdicts;
 	uint32_t ablate;              /* diagnostics only (XFG_ABLATE env), 0 in production:
 				       * 2 = no counter atomics, 4 = stage only (no parse) */
+	uint32_t pad;
 };
 
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
@@ -113,6 +134,21 @@ XFG_HD uint32_t xfg_hash_eth(uint64_t mac, uint32_t seed)
 XFG_HD uint32_t xfg_home(uint32_t h, uint32_t nbuckets)
 {
 	return (uint32_t)(((uint64_t)h * nbuckets) >> 32);
+}
+
+/* Bloom filter: word index from the key hash h (a different range
+ * reduction than the bucket's: the high-multiply of a re-mixed value), and
+ * XFG_BLOOM_K bit positions from a second finaliser round. */
+XFG_HD uint32_t xfg_bloom_word(uint32_t h, uint32_t nwords)
+{
+	return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * nwords) >> 32);
+}
+
+XFG_HD unsigned long long xfg_bloom_mask(uint32_t h)
+{
+	uint32_t g = xfg_fmix32(h ^ 0x7f4a7c15u);
+	return (1ull << (g & 63)) | (1ull << ((g >> 6) & 63)) | (1ull << ((g >> 12) & 63)) |
+	       (1ull << ((g >> 18) & 63));
 }
 
 #endif /* XFG_LAYOUT_H */

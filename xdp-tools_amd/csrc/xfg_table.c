@@ -6,16 +6,14 @@
 #include <stdlib.h>
 #include <string.h>
 
-/* Target load factors per key type (slots per 64-byte bucket 16 / 4 / 8):
- * with 16-slot buckets at 0.66 ~2% of buckets overflow at full capacity. */
+/* Target load factors per key type (slots per bucket 12 / 3 / 6): with
+ * 12-slot buckets at 0.6 about 3% of buckets overflow at full capacity. */
 static uint32_t buckets_for(uint32_t capacity, uint32_t spb)
 {
-	double lf = spb >= 16 ? 0.66 : (spb >= 8 ? 0.6 : 0.5);
+	double lf = spb >= 12 ? 0.6 : (spb >= 6 ? 0.55 : 0.45);
 	uint64_t nb = (uint64_t)((double)capacity / (spb * lf)) + 1;
-	if (nb < 1)
-		nb = 1;
-	if (nb > 0x7fffffffull / spb)
-		nb = 0x7fffffffull / spb;
+	if (nb > 0x7fffffffull / spb - 1)
+		nb = 0x7fffffffull / spb - 1;
 	return (uint32_t)nb;
 }
 
@@ -35,9 +33,12 @@ int xfg_table_init(struct xfg_table *t, uint32_t keylen, uint32_t capacity, uint
 	t->seed = seed;
 	t->nbuckets = buckets_for(capacity, t->slots_per_bucket);
 	t->nslots = t->nbuckets * t->slots_per_bucket;
-	t->keys = calloc(t->nbuckets, XFG_BUCKET_BYTES);
-	t->meta = calloc(t->nbuckets, 1);
-	if (!t->keys || !t->meta) {
+	/* ~12 filter bits per key: a 1M-rule filter is 1.5 MB (L2-resident) */
+	uint64_t words = ((uint64_t)capacity * 12 + 63) / 64;
+	t->bloom_words = (uint32_t)(words < 16 ? 16 : words);
+	t->img = calloc(xfg_table_img_bytes(t), 1);
+	t->bloom = calloc(t->bloom_words, 8);
+	if (!t->img || !t->bloom) {
 		xfg_table_free(t);
 		return -ENOMEM;
 	}
@@ -46,13 +47,12 @@ int xfg_table_init(struct xfg_table *t, uint32_t keylen, uint32_t capacity, uint
 
 void xfg_table_free(struct xfg_table *t)
 {
-	free(t->keys);
-	free(t->meta);
-	t->keys = NULL;
-	t->meta = NULL;
+	free(t->img);
+	free(t->bloom);
+	t->img = NULL;
+	t->bloom = NULL;
 }
 
-/* Stored form of a user key (zero-padded to slot_bytes). */
 static void stored_key(const struct xfg_table *t, const void *key, uint8_t *out)
 {
 	memset(out, 0, 16);
@@ -67,29 +67,27 @@ static int is_zero(const uint8_t *k, uint32_t n)
 	return 1;
 }
 
-static uint32_t home_bucket(const struct xfg_table *t, const uint8_t *sk)
+static uint32_t key_hash(const struct xfg_table *t, const uint8_t *sk)
 {
-	uint32_t h;
 	if (t->keylen == 4) {
 		uint32_t k;
 		memcpy(&k, sk, 4);
-		h = xfg_hash_v4(k, t->seed);
+		return xfg_hash_v4(k, t->seed);
 	} else if (t->keylen == 16) {
 		uint32_t w[4];
 		memcpy(w, sk, 16);
-		h = xfg_hash_v6(w[0], w[1], w[2], w[3], t->seed);
-	} else {
-		uint64_t m;
-		memcpy(&m, sk, 8);
-		h = xfg_hash_eth(m, t->seed);
+		return xfg_hash_v6(w[0], w[1], w[2], w[3], t->seed);
 	}
-	return xfg_home(h, t->nbuckets);
+	uint64_t m;
+	memcpy(&m, sk, 8);
+	return xfg_hash_eth(m, t->seed);
 }
 
-static inline uint8_t *slot_ptr(const struct xfg_table *t, uint64_t slot)
+static inline uint32_t meta_of(const struct xfg_table *t, uint32_t b)
 {
-	uint64_t b = slot / t->slots_per_bucket, i = slot % t->slots_per_bucket;
-	return t->keys + b * XFG_BUCKET_BYTES + i * t->slot_bytes;
+	uint32_t m;
+	memcpy(&m, t->img + (uint64_t)b * XFG_BUCKET_BYTES + XFG_META_OFF, 4);
+	return m;
 }
 
 int64_t xfg_table_find(const struct xfg_table *t, const void *key)
@@ -100,25 +98,35 @@ int64_t xfg_table_find(const struct xfg_table *t, const void *key)
 		return t->zero_present ? (int64_t)t->nslots : -1;
 	if (!t->count)
 		return -1;
-	uint32_t b = home_bucket(t, sk);
+	uint32_t b = xfg_home(key_hash(t, sk), t->nbuckets);
 	for (uint32_t d = 0; d <= t->max_disp; d++) {
 		uint32_t bb = b + d;
 		while (bb >= t->nbuckets)
 			bb -= t->nbuckets;
-		const uint8_t *bk = t->keys + (uint64_t)bb * XFG_BUCKET_BYTES;
+		const uint8_t *bk = t->img + (uint64_t)bb * XFG_BUCKET_BYTES;
 		for (uint32_t i = 0; i < t->slots_per_bucket; i++)
 			if (!memcmp(bk + i * t->slot_bytes, sk, t->slot_bytes))
 				return (int64_t)bb * t->slots_per_bucket + i;
-		if (!(t->meta[bb] & XFG_META_OVERFLOW))
+		if (!(meta_of(t, bb) & XFG_META_OVERFLOW))
 			return -1;
 	}
 	return -1;
 }
 
+static uint32_t bloom_add(struct xfg_table *t, uint32_t h)
+{
+	uint32_t w = xfg_bloom_word(h, t->bloom_words);
+	t->bloom[w] |= xfg_bloom_mask(h);
+	return w;
+}
+
 int64_t xfg_table_insert(struct xfg_table *t, const void *key,
-			 void (*meta_changed)(void *arg, uint32_t bucket), void *arg)
+			 void (*meta_changed)(void *arg, uint32_t bucket), void *arg,
+			 int64_t *bloom_word)
 {
 	uint8_t sk[16];
+	if (bloom_word)
+		*bloom_word = -1;
 	if (t->count >= t->capacity)
 		return -E2BIG;
 	stored_key(t, key, sk);
@@ -127,23 +135,29 @@ int64_t xfg_table_insert(struct xfg_table *t, const void *key,
 		t->count++;
 		return t->nslots;
 	}
-	uint32_t b = home_bucket(t, sk);
+	uint32_t h = key_hash(t, sk);
+	uint32_t b = xfg_home(h, t->nbuckets);
 	for (uint32_t d = 0; d < t->nbuckets; d++) {
 		uint32_t bb = b + d;
 		while (bb >= t->nbuckets)
 			bb -= t->nbuckets;
-		uint8_t *bk = t->keys + (uint64_t)bb * XFG_BUCKET_BYTES;
+		uint8_t *bk = t->img + (uint64_t)bb * XFG_BUCKET_BYTES;
 		for (uint32_t i = 0; i < t->slots_per_bucket; i++) {
 			if (is_zero(bk + i * t->slot_bytes, t->slot_bytes)) {
 				memcpy(bk + i * t->slot_bytes, sk, t->slot_bytes);
 				if (d > t->max_disp)
 					t->max_disp = d;
 				t->count++;
+				uint32_t w = bloom_add(t, h);
+				if (bloom_word)
+					*bloom_word = w;
 				return (int64_t)bb * t->slots_per_bucket + i;
 			}
 		}
-		if (!(t->meta[bb] & XFG_META_OVERFLOW)) {
-			t->meta[bb] |= XFG_META_OVERFLOW;
+		uint32_t m = meta_of(t, bb);
+		if (!(m & XFG_META_OVERFLOW)) {
+			m |= XFG_META_OVERFLOW;
+			memcpy(bk + XFG_META_OFF, &m, 4);
 			if (meta_changed)
 				meta_changed(arg, bb);
 		}
@@ -158,10 +172,28 @@ int64_t xfg_table_remove(struct xfg_table *t, const void *key)
 		return -ENOENT;
 	if ((uint64_t)s == t->nslots)
 		t->zero_present = 0;
-	else
-		memset(slot_ptr(t, s), 0, t->slot_bytes);
+	else {
+		memset(t->img + xfg_table_key_off(t, s), 0, t->slot_bytes);
+		t->bloom_stale++;
+	}
 	t->count--;
 	return s;
+}
+
+int xfg_table_bloom_needs_rebuild(const struct xfg_table *t)
+{
+	return t->bloom_stale > 64 && t->bloom_stale * 4 > t->count;
+}
+
+void xfg_table_bloom_rebuild(struct xfg_table *t)
+{
+	memset(t->bloom, 0, (size_t)t->bloom_words * 8);
+	for (uint64_t s = 0; s < t->nslots; s++) {
+		const uint8_t *k = t->img + xfg_table_key_off(t, s);
+		if (!is_zero(k, t->slot_bytes))
+			bloom_add(t, key_hash(t, k));
+	}
+	t->bloom_stale = 0;
 }
 
 int xfg_table_slot_key(const struct xfg_table *t, uint64_t slot, void *out)
@@ -174,7 +206,7 @@ int xfg_table_slot_key(const struct xfg_table *t, uint64_t slot, void *out)
 	}
 	if (slot > t->nslots)
 		return -ENOENT;
-	const uint8_t *p = slot_ptr(t, slot);
+	const uint8_t *p = t->img + xfg_table_key_off(t, slot);
 	if (is_zero(p, t->slot_bytes))
 		return -ENOENT;
 	memcpy(out, p, t->keylen);
@@ -184,7 +216,7 @@ int xfg_table_slot_key(const struct xfg_table *t, uint64_t slot, void *out)
 int64_t xfg_table_next_slot(const struct xfg_table *t, int64_t after)
 {
 	for (uint64_t s = (uint64_t)(after + 1); s < t->nslots; s++)
-		if (!is_zero(slot_ptr(t, s), t->slot_bytes))
+		if (!is_zero(t->img + xfg_table_key_off(t, s), t->slot_bytes))
 			return (int64_t)s;
 	if ((uint64_t)(after + 1) <= t->nslots && t->zero_present)
 		return t->nslots;
@@ -199,4 +231,5 @@ void xfg_table_desc(const struct xfg_table *t, struct xfg_tdesc *d)
 	d->zero_present = t->zero_present;
 	d->nslots = t->nslots;
 	d->seed = t->seed;
+	d->bloom_words = t->bloom_words;
 }

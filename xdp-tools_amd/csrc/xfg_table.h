@@ -1,9 +1,10 @@
 /* SPDX-License-Identifier: GPL-2.0 */
 /* xfg_table.h — host image of one device hash table (layout: xfg_layout.h).
  *
- * The host owns the key image (identical on every device, so slot indices
- * agree across devices and the counter arrays can be reduced element-wise);
- * per-device values (flags, hits) live on the devices only.
+ * The host owns the key bytes and overflow bits of every bucket (identical
+ * on every device, so slot indices agree across devices and the counter
+ * arrays can be reduced element-wise) and the Bloom prefilter; per-device
+ * values (flag bytes inside the buckets, the hits array) live on the devices.
  */
 #ifndef XFG_TABLE_H
 #define XFG_TABLE_H
@@ -15,15 +16,17 @@ struct xfg_table {
 	uint32_t keylen;      /* user key bytes: 4, 16 or 6 */
 	uint32_t slot_bytes;  /* stored key bytes: 4, 16 or 8 */
 	uint32_t slots_per_bucket;
-	uint32_t nbuckets;
-	uint32_t nslots;      /* nbuckets * slots_per_bucket */
+	uint32_t nbuckets;    /* hashed buckets; bucket nbuckets holds the zero key */
+	uint32_t nslots;      /* nbuckets * slots_per_bucket (= slot of the zero key) */
 	uint32_t capacity;    /* max keys (the reference's max_entries) */
 	uint32_t count;
 	uint32_t max_disp;
 	uint32_t zero_present;
 	uint32_t seed;
-	uint8_t *keys;        /* nbuckets * 64 bytes */
-	uint8_t *meta;        /* nbuckets bytes */
+	uint32_t bloom_words;
+	uint32_t bloom_stale; /* deletes since the filter was last rebuilt */
+	uint8_t *img;         /* (nbuckets + 1) * 64 bytes: keys + meta, flags zero */
+	unsigned long long *bloom;
 };
 
 /* keylen 4 (ipv4), 16 (ipv6), 6 (ethernet). Returns 0 or -ENOMEM/-EINVAL. */
@@ -34,14 +37,20 @@ void xfg_table_free(struct xfg_table *t);
 int64_t xfg_table_find(const struct xfg_table *t, const void *key);
 
 /* Insert @key (must be absent): returns its slot, or -E2BIG when count ==
- * capacity.  *touched_bucket (if not NULL) receives the bucket whose key
- * bytes changed (-1 for the zero key); every bucket whose meta changed is
- * reported through the optional callback. */
+ * capacity.  Buckets whose meta word changed are reported through the
+ * optional callback; the Bloom word that changed is returned in *bloom_word
+ * (or -1 for the zero key). */
 int64_t xfg_table_insert(struct xfg_table *t, const void *key,
-			 void (*meta_changed)(void *arg, uint32_t bucket), void *arg);
+			 void (*meta_changed)(void *arg, uint32_t bucket), void *arg,
+			 int64_t *bloom_word);
 
 /* Remove @key: returns its former slot, or -ENOENT. */
 int64_t xfg_table_remove(struct xfg_table *t, const void *key);
+
+/* True when deletes have left enough stale Bloom bits that a rebuild pays. */
+int xfg_table_bloom_needs_rebuild(const struct xfg_table *t);
+/* Recompute the Bloom filter from the keys present. */
+void xfg_table_bloom_rebuild(struct xfg_table *t);
 
 /* Copy the user-visible key stored in @slot to @out; returns 0, or -ENOENT
  * if the slot is empty. */
@@ -50,6 +59,22 @@ int xfg_table_slot_key(const struct xfg_table *t, uint64_t slot, void *out);
 /* Iteration in slot order (zero-key slot last): first slot > @after that
  * holds a key (after = -1 to start), or -1 when exhausted. */
 int64_t xfg_table_next_slot(const struct xfg_table *t, int64_t after);
+
+/* Byte offsets inside the bucket image of a slot's key and flag byte. */
+static inline uint64_t xfg_table_key_off(const struct xfg_table *t, uint64_t slot)
+{
+	return (slot / t->slots_per_bucket) * XFG_BUCKET_BYTES +
+	       (slot % t->slots_per_bucket) * t->slot_bytes;
+}
+static inline uint64_t xfg_table_flag_off(const struct xfg_table *t, uint64_t slot)
+{
+	return (slot / t->slots_per_bucket) * XFG_BUCKET_BYTES + XFG_FLAGS_OFF +
+	       (slot % t->slots_per_bucket);
+}
+static inline uint64_t xfg_table_img_bytes(const struct xfg_table *t)
+{
+	return ((uint64_t)t->nbuckets + 1) * XFG_BUCKET_BYTES;
+}
 
 /* Descriptor for the kernel (device pointers filled by the caller). */
 void xfg_table_desc(const struct xfg_table *t, struct xfg_tdesc *d);
