@@ -372,19 +372,21 @@ __device__ __forceinline__ Hit probe_chain(const xfg_tdesc &t, uint32_t b, uint3
 	return { -1, 0 };
 }
 
-// A pending lookup: hash computed, Bloom word tested, bucket line loaded.
+// A pending lookup: hash computed and Bloom word tested.  The Bloom words of
+// all keys of a stage are loaded together (8 bytes each, L2-resident); the
+// bucket line is fetched only for a key the filter passes, one at a time,
+// which keeps a single 64-byte line live per lane.
 template <int KIND>
 struct Probe {
 	uint32_t k0, k1, k2, k3;
 	uint32_t b;
 	bool zero, live;
-	Line l;
 
 	__device__ __forceinline__ void start(const xfg_tdesc &t, bool want, uint32_t a0,
 					      uint32_t a1 = 0, uint32_t a2 = 0, uint32_t a3 = 0)
 	{
 		k0 = a0; k1 = a1; k2 = a2; k3 = a3;
-		zero = (a0 | a1 | a2 | a3) == 0;
+		zero = want && (a0 | a1 | a2 | a3) == 0;
 		live = false;
 		b = 0;
 		if (!want || zero)
@@ -399,19 +401,13 @@ struct Probe {
 		b = xfg_home(h, t.nbuckets);
 		live = bloom_maybe(t, h);
 	}
-	__device__ __forceinline__ void fetch(const xfg_tdesc &t)
+	__device__ __forceinline__ Hit result(const xfg_tdesc &t) const
 	{
-		if (live)
-			l = load_line(t, b);
-	}
-	__device__ __forceinline__ Hit result(const xfg_tdesc &t, bool want) const
-	{
-		if (!want)
-			return { -1, 0 };
 		if (zero)
 			return zero_hit(t);
 		if (!live)
 			return { -1, 0 };
+		const Line l = load_line(t, b);
 		const int i = match<KIND>(l, k0, k1, k2, k3);
 		if (i >= 0)
 			return { (int64_t)b * slots_of<KIND>() + i, l.flag(i) };
@@ -421,36 +417,51 @@ struct Probe {
 	}
 };
 
+// Counter identity of a hit: map id in the top two bits, slot below
+// (slots < 2^30 for every capacity the host accepts).
+constexpr uint32_t CT_NONE = 0xffffffffu;
+constexpr uint32_t CT_V4 = 0u << 30, CT_V6 = 1u << 30, CT_ETH = 2u << 30, CT_PORT = 3u << 30;
+
+__device__ __forceinline__ unsigned long long *counter_ptr(const xfg_kargs &a, uint32_t tag)
+{
+	const uint32_t slot = tag & 0x3fffffffu;
+	switch (tag >> 30) {
+	case 0: return a.t4.hits + slot;
+	case 1: return a.t6.hits + slot;
+	case 2: return a.te.hits + slot;
+	default: return a.port_hits + slot;
+	}
+}
+
 // CHECK_MAP (xdp-filter/xdpfilt_prog.h:56-64): hit iff the key exists and
 // (value & mask) == mask; the counter bump is deferred to the caller.
-__device__ __forceinline__ bool take(const xfg_tdesc &t, const Hit &h, uint32_t mask,
-				     unsigned long long *&hitp)
+__device__ __forceinline__ bool take(const Hit &h, uint32_t mask, uint32_t ct, uint32_t &tag)
 {
 	if (h.slot >= 0 && (h.flags & mask) == mask) {
-		hitp = t.hits + h.slot;
+		tag = ct | (uint32_t)h.slot;
 		return true;
 	}
 	return false;
 }
 
 __device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s_pbits,
-					   uint32_t key, uint32_t mask, unsigned long long *&hitp)
+					   uint32_t key, uint32_t mask, uint32_t &tag)
 {
 	if (!((s_pbits[key >> 5] >> (key & 31)) & 1))
 		return false;
 	if ((a.port_flags[key] & mask) == mask) {
-		hitp = a.port_hits + key;
+		tag = CT_PORT | key;
 		return true;
 	}
 	return false;
 }
 
 // ---------------------------------------------------------------- the program
-// Ordered lookups over a parsed packet; returns the xdp action and sets hitp
-// to the first matching rule's counter.
+// Ordered lookups over a parsed packet; returns the xdp action and sets tag
+// to the first matching rule's counter identity (CT_NONE if none).
 template <uint32_t FEAT, int W>
 __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p, const Parsed &r,
-					    const uint32_t *s_pbits, unsigned long long *&hitp)
+					    const uint32_t *s_pbits, uint32_t &tag)
 {
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;   // VERDICT_HIT
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;  // VERDICT_MISS
@@ -464,10 +475,8 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 			Probe<2> d, s;
 			d.start(a.te, true, p.u32(0), p.raw16(4));
 			s.start(a.te, true, p.u32(6), p.raw16(10));
-			d.fetch(a.te);
-			s.fetch(a.te);
-			if (take(a.te, d.result(a.te, true), M_DST, hitp) ||
-			    take(a.te, s.result(a.te, true), M_SRC, hitp))
+			if (take(d.result(a.te), M_DST, CT_ETH, tag) ||
+			    take(s.result(a.te), M_SRC, CT_ETH, tag))
 				return HIT;
 		}
 	}
@@ -483,12 +492,10 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 			Probe<4> x, y;
 			x.start(a.t4, true, r.k4a);
 			y.start(a.t4, want_b, r.k4b);
-			x.fetch(a.t4);
-			y.fetch(a.t4);
 			const uint32_t mx = arp ? M_SRC : M_DST;
 			const uint32_t my = arp ? (r.arp_op == 1 ? M_DST : M_SRC) : M_SRC;
-			if (take(a.t4, x.result(a.t4, true), mx, hitp) ||
-			    take(a.t4, y.result(a.t4, want_b), my, hitp))
+			if (take(x.result(a.t4), mx, CT_V4, tag) ||
+			    (want_b && take(y.result(a.t4), my, CT_V4, tag)))
 				return HIT;
 		}
 	}
@@ -499,10 +506,8 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 			Probe<6> d, s;
 			d.start(a.t6, true, p.u32(o + 24), p.u32(o + 28), p.u32(o + 32), p.u32(o + 36));
 			s.start(a.t6, true, p.u32(o + 8), p.u32(o + 12), p.u32(o + 16), p.u32(o + 20));
-			d.fetch(a.t6);
-			s.fetch(a.t6);
-			if (take(a.t6, d.result(a.t6, true), M_DST, hitp) ||
-			    take(a.t6, s.result(a.t6, true), M_SRC, hitp))
+			if (take(d.result(a.t6), M_DST, CT_V6, tag) ||
+			    take(s.result(a.t6), M_SRC, CT_V6, tag))
 				return HIT;
 		}
 	}
@@ -514,8 +519,7 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 			const uint32_t o = r.ond;
 			Probe<6> t;
 			t.start(a.t6, true, p.u32(o), p.u32(o + 4), p.u32(o + 8), p.u32(o + 12));
-			t.fetch(a.t6);
-			if (take(a.t6, t.result(a.t6, true), r.nd == 135 ? M_DST : M_SRC, hitp))
+			if (take(t.result(a.t6), r.nd == 135 ? M_DST : M_SRC, CT_V6, tag))
 				return HIT;
 		}
 	}
@@ -525,12 +529,34 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 		if (a.port_count && r.l4proto) {
 			// lookup_verdict_udp / _tcp (xdpfilt_prog.h:92-101 / :76-85)
 			const uint32_t pm = r.l4proto == 17 ? M_UDP : M_TCP;
-			if (check_port(a, s_pbits, r.pdst, M_DST | pm, hitp) ||
-			    check_port(a, s_pbits, r.psrc, M_SRC | pm, hitp))
+			if (check_port(a, s_pbits, r.pdst, M_DST | pm, tag) ||
+			    check_port(a, s_pbits, r.psrc, M_SRC | pm, tag))
 				return HIT;
 		}
 	}
 	return MISS;
+}
+
+// Per-workgroup counter cache in LDS: direct-mapped on the counter identity.
+// A rule hit by many packets (a hot port, an attacked address) is summed
+// here and reaches memory once per workgroup; a slot already owned by a
+// different counter sends the bump straight to its global atomic.
+constexpr int CC_ENTRIES = 1024;
+
+__device__ __forceinline__ void count_hit(const xfg_kargs &a, uint32_t *s_ctag, uint32_t *s_ccnt,
+					  uint32_t tag, uint32_t n)
+{
+	const uint32_t e = (tag * 0x9E3779B1u) >> 22;   // 10 bits
+	uint32_t t = s_ctag[e];
+	if (t == CT_NONE) {
+		t = atomicCAS(&s_ctag[e], CT_NONE, tag);
+		if (t == CT_NONE)
+			t = tag;
+	}
+	if (t == tag)
+		atomicAdd(&s_ccnt[e], n);
+	else
+		atomicAdd(counter_ptr(a, tag), (unsigned long long)n);
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -561,12 +587,17 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	__shared__ uint32_t win[TILE * ROWDW];
 	__shared__ uint32_t s_pbits[PORTS ? 2048 : 1];
+	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
 	__shared__ unsigned long long s_stats[6];
 
 	const int tid = threadIdx.x;
 	const int lane = tid & 63;
 	if (tid < 6)
 		s_stats[tid] = 0;
+	for (int i = tid; i < CC_ENTRIES; i += TILE) {
+		s_ctag[i] = CT_NONE;
+		s_ccnt[i] = 0;
+	}
 	if constexpr (PORTS) {
 		if (a.port_count)
 			for (int i = tid; i < 2048; i += TILE)
@@ -618,38 +649,38 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 		// 2-4. parse, match, verdict
 		const uint64_t gi = base + tid;
 		uint32_t act = A_NONE;
-		unsigned long long *hitp = nullptr;
+		uint32_t tag = CT_NONE;
 		if (gi < a.n) {
 			Pkt<W> p{ &win[tid * ROWDW], pkt_ptr(a, gi), len };
 			if (a.ablate & 4) {
 				act = p.u8(0) & 1;
 			} else {
 				const Parsed r = parse<FEAT, W>(p);
-				act = lookups<FEAT, W>(a, p, r, s_pbits, hitp);
+				act = lookups<FEAT, W>(a, p, r, s_pbits, tag);
 			}
 			a.verdicts[gi] = (uint8_t)act;
 		}
 		if (a.ablate & 2)
-			hitp = nullptr;
+			tag = CT_NONE;
 
-		// counter bump, aggregated over same-slot lanes of the wave
+		// counter bump: lanes of the wave hitting the same rule are merged
+		// (two leader rounds), then summed in the LDS counter cache
 #pragma unroll 1
-		for (int rnd = 0; rnd < 4; rnd++) {
-			const unsigned long long pend = __ballot(hitp != nullptr);
+		for (int rnd = 0; rnd < 2; rnd++) {
+			const unsigned long long pend = __ballot(tag != CT_NONE);
 			if (!pend)
 				break;
 			const int leader = __ffsll((long long)pend) - 1;
-			const unsigned long long lp = __shfl((unsigned long long)(uintptr_t)hitp, leader);
-			const bool mine = (unsigned long long)(uintptr_t)hitp == lp;
+			const uint32_t lt = __shfl(tag, leader);
+			const bool mine = tag == lt;
 			const unsigned long long same = __ballot(mine);
 			if (lane == leader)
-				atomicAdd(reinterpret_cast<unsigned long long *>(lp),
-					  (unsigned long long)__popcll(same));
+				count_hit(a, s_ctag, s_ccnt, lt, (uint32_t)__popcll(same));
 			if (mine)
-				hitp = nullptr;
+				tag = CT_NONE;
 		}
-		if (hitp)
-			atomicAdd(hitp, 1ull);
+		if (tag != CT_NONE)
+			count_hit(a, s_ctag, s_ccnt, tag, 1);
 
 		// 5. per-action stats (xdp_stats_record_action)
 #pragma unroll
@@ -665,6 +696,9 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 	}
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
+	for (int i = tid; i < CC_ENTRIES; i += TILE)
+		if (s_ctag[i] != CT_NONE && s_ccnt[i])
+			atomicAdd(counter_ptr(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
 }
 
 template <uint32_t FEAT>

@@ -33,6 +33,8 @@ int xfg_table_init(struct xfg_table *t, uint32_t keylen, uint32_t capacity, uint
 	t->seed = seed;
 	t->nbuckets = buckets_for(capacity, t->slots_per_bucket);
 	t->nslots = t->nbuckets * t->slots_per_bucket;
+	if (t->nslots >= (1u << 30))   /* kernel counter tags carry 30-bit slots */
+		return -E2BIG;
 	/* ~12 filter bits per key: a 1M-rule filter is 1.5 MB (L2-resident) */
 	uint64_t words = ((uint64_t)capacity * 12 + 63) / 64;
 	t->bloom_words = (uint32_t)(words < 16 ? 16 : words);
