@@ -30,17 +30,32 @@ def main():
     ap.add_argument("--log2-packets", type=int, default=24)
     ap.add_argument("--rules", type=int, default=1_000_000)
     ap.add_argument("--masks", default="0,2,1,4")
+    ap.add_argument("--envs", default="",
+                    help="';'-separated variants, each 'K=V,K=V' (diagnostic env knobs), "
+                         "timed with mask 0; e.g. 'XFG_MINW=5;XFG_GRID_PER_CU=4'")
     a = ap.parse_args()
     a.cpu_seconds, a.no_cpu = 0, True
     f, (d_data, d_lens, d_verd), n, stride, lens, alg, _, _, _ = bench.setup(a, 0, 0)
-    masks = [int(m) for m in a.masks.split(",")]
-    res = {m: [] for m in masks}
+    variants = [("mask", int(m), {}) for m in a.masks.split(",") if m != ""]
+    for v in a.envs.split(";"):
+        if v.strip():
+            kv = dict(x.split("=") for x in v.split(","))
+            variants.append(("env", v, kv))
+    res = {str(v[1]): [] for v in variants}
+    knobs = {"XFG_ABLATE", "XFG_VARIANT", "XFG_GRID_PER_CU"}
     for _ in range(a.rounds):
-        for m in masks:
-            os.environ["XFG_ABLATE"] = str(m)
-            res[m].append(f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr,
-                                           a.iters, lens_u16=True))
-    os.environ["XFG_ABLATE"] = "0"
+        for kind, key, kv in variants:
+            for k in knobs:
+                os.environ.pop(k, None)
+            if kind == "mask":
+                os.environ["XFG_ABLATE"] = str(key)
+            else:
+                os.environ.update(kv)
+            res[str(key)].append(f.classify_timed(d_data.ptr, d_lens.ptr, n, stride,
+                                                  d_verd.ptr, a.iters, lens_u16=True))
+    for k in knobs:
+        os.environ.pop(k, None)
+    masks = list(res)
     out = {}
     for m in masks:
         ts = sorted(res[m])

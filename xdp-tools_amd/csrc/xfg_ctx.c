@@ -31,6 +31,7 @@ int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a, unsig
 			void *stream);
 int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sink, unsigned grid,
 			   void *stream);
+int xfg_classify_occupancy(uint32_t prog_features, uint32_t window);
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
 #define PORT_BITS_WORDS (XFG_PORT_MAP_ENTRIES / 32)
@@ -55,6 +56,8 @@ struct xfg_dev {
 	unsigned long long *stats;      /* 10 */
 	unsigned long long *red_stats;  /* 10 */
 	void *sink;                     /* stream-read probe sink */
+	int occ64, occ128, occ_st;      /* resident classify workgroups per CU */
+	hipEvent_t ev_user, ev_done;    /* ordering against a caller's stream */
 };
 
 struct xfg_ctx {
@@ -70,6 +73,12 @@ struct xfg_ctx {
 	uint8_t *port_flags_host;        /* OR over devices of the port flags */
 	uint32_t *port_bits_host;        /* bit set <=> port_flags_host != 0 */
 	uint32_t port_count;
+	/* flag-bit census: flag_or[map][slot] = OR over devices of the slot's
+	 * flag byte; flag_cnt[map][bit] = slots with that bit (likewise for the
+	 * ports).  The kernel skips a lookup whose mask no key carries. */
+	uint8_t *flag_or[NMAPS_HASH];
+	uint32_t flag_cnt[NMAPS_HASH][8];
+	uint32_t port_flag_cnt[8];
 	/* multi-process reduction */
 	ncclComm_t comm;
 	int comm_ready;
@@ -163,6 +172,10 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->stats);
 	hipFree(d->red_stats);
 	hipFree(d->sink);
+	if (d->ev_user)
+		hipEventDestroy(d->ev_user);
+	if (d->ev_done)
+		hipEventDestroy(d->ev_done);
 	if (d->ev0)
 		hipEventDestroy(d->ev0);
 	if (d->ev1)
@@ -201,6 +214,11 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	HIPCHK(hipMalloc((void **)&d->stats, 10 * 8));
 	HIPCHK(hipMemset(d->stats, 0, 10 * 8));
 	HIPCHK(hipMalloc(&d->sink, 16 * 65536));
+	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
+	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
+	d->occ64 = xfg_classify_occupancy(ctx->prog_features, 64);
+	d->occ128 = xfg_classify_occupancy(ctx->prog_features, 128);
+	d->occ_st = xfg_classify_occupancy(ctx->prog_features, 1);
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -231,6 +249,13 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 	    (err = xfg_table_init(&ctx->t[1], 16, cap6, seed ^ 0x6a09e667u)) ||
 	    (err = xfg_table_init(&ctx->t[2], 6, cape, seed ^ 0xbb67ae85u)))
 		goto fail;
+	for (int i = 0; i < NMAPS_HASH; i++) {
+		ctx->flag_or[i] = calloc((size_t)ctx->t[i].nslots + 1, 1);
+		if (!ctx->flag_or[i]) {
+			err = -ENOMEM;
+			goto fail;
+		}
+	}
 	ctx->port_flags_host = calloc(XFG_PORT_MAP_ENTRIES, 1);
 	ctx->port_bits_host = calloc(PORT_BITS_WORDS, 4);
 	if (!ctx->port_flags_host || !ctx->port_bits_host) {
@@ -292,6 +317,7 @@ void xfg_close(xfg_ctx *ctx)
 	for (int i = 0; i < NMAPS_HASH; i++) {
 		xfg_table_free(&ctx->t[i]);
 		free(ctx->host_vals[i]);
+		free(ctx->flag_or[i]);
 	}
 	free(ctx->host_port_vals);
 	free(ctx->port_flags_host);
@@ -352,8 +378,35 @@ static int slot_values(xfg_ctx *ctx, int mi, uint64_t slot, uint64_t *vals)
 	return 0;
 }
 
+static void census(uint32_t *cnt, uint8_t old, uint8_t f)
+{
+	for (int b = 0; b < 8; b++) {
+		cnt[b] -= (old >> b) & 1;
+		cnt[b] += (f >> b) & 1;
+	}
+}
+
+static uint32_t census_mask(const uint32_t *cnt)
+{
+	uint32_t m = 0;
+	for (int b = 0; b < 8; b++)
+		if (cnt[b])
+			m |= 1u << b;
+	return m;
+}
+
+static void flags_note(xfg_ctx *ctx, int mi, uint64_t slot, uint8_t f)
+{
+	census(ctx->flag_cnt[mi], ctx->flag_or[mi][slot], f);
+	ctx->flag_or[mi][slot] = f;
+}
+
 static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals)
 {
+	uint8_t any = 0;
+	for (int i = 0; i < (ctx->ndev ? ctx->ndev : 1); i++)
+		any |= vals[i] & 63;
+	flags_note(ctx, mi, slot, any);
 	if (!ctx->ndev) {
 		ctx->host_vals[mi][slot] = vals[0];
 		return 0;
@@ -422,6 +475,7 @@ static int port_key(const void *key, uint32_t *k)
  * skip) and the 65536-bit bitmap the kernel stages in LDS. */
 static int port_flags_note(xfg_ctx *ctx, uint32_t k, uint8_t f)
 {
+	census(ctx->port_flag_cnt, ctx->port_flags_host[k], f);
 	if (!ctx->port_flags_host[k] && f)
 		ctx->port_count++;
 	else if (ctx->port_flags_host[k] && !f)
@@ -752,6 +806,7 @@ int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t
 			err = (int)s;
 			break;
 		}
+		flags_note(ctx, mi, (uint64_t)s, vals[i] & 63);
 		if (nd) {
 			for (int d = 0; d < nd; d++) {
 				img[ib * d + xfg_table_flag_off(t, s)] = vals[i] & 63;
@@ -797,7 +852,15 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 		td[i]->buckets = d->m[i].buckets;
 		td[i]->bloom = d->m[i].bloom;
 		td[i]->hits = d->m[i].hits;
+		td[i]->fmask = census_mask(ctx->flag_cnt[i]);
 	}
+	a->port_fmask = census_mask(ctx->port_flag_cnt);
+	uint64_t gb = 0;
+	for (int i = 0; i < NMAPS_HASH; i++) {
+		a->gbase[i] = (uint32_t)gb;
+		gb += (uint64_t)ctx->t[i].nslots + 1;
+	}
+	a->gbase[3] = (uint32_t)gb;
 	a->port_flags = d->port_flags;
 	a->port_bits = d->port_bits;
 	a->port_hits = d->port_hits;
@@ -814,9 +877,21 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 	 * stride; everything else stages 128 bytes (every synthetic class and all
 	 * common headers parse within 78 bytes; longer chains read HBM). */
 	a->window = (!b->offsets && b->stride && b->stride <= 64) ? 64 : 128;
+	/* The streamed kernel takes every fixed-stride batch whose 64-byte
+	 * windows and 16-byte length chunks can be DMA'd whole (headers past
+	 * byte 64 are read from HBM by the few packets that have them). */
+	a->streamed = !b->offsets && b->stride >= 64 && !((uintptr_t)b->lens & 15);
+	const char *ks = getenv("XFG_KERNEL");    /* diagnostics only */
+	if (ks && !strcmp(ks, "classic"))
+		a->streamed = 0;
+	if (a->streamed)
+		a->window = 64;
 	/* Diagnostics only: XFG_ABLATE=<mask> (1 = treat every table as empty,
 	 * 2 = drop counter atomics, 4 = stage windows only).  Results are wrong
 	 * under any non-zero mask; tools/ablate.py uses it to split time. */
+	const char *mw = getenv("XFG_VARIANT");
+	if (mw && *mw)
+		a->variant = (uint32_t)strtoul(mw, NULL, 0);
 	const char *ab = getenv("XFG_ABLATE");
 	if (ab && *ab) {
 		a->ablate = (uint32_t)strtoul(ab, NULL, 0);
@@ -827,13 +902,44 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 	}
 }
 
-static unsigned grid_for(const struct xfg_dev *d, uint64_t n)
+/* One persistent wave of workgroups: every resident slot of every CU. */
+static unsigned grid_for(const struct xfg_dev *d, const struct xfg_kargs *a)
 {
-	uint64_t tiles = (n + 255) / 256;
-	uint64_t cap = (uint64_t)d->ncu * 8;
+	uint64_t tiles = (a->n + 255) / 256;
+	uint64_t per_cu = a->streamed ? d->occ_st : a->window <= 64 ? d->occ64 : d->occ128;
+	const char *g = getenv("XFG_GRID_PER_CU");   /* diagnostics only */
+	if (g && *g)
+		per_cu = strtoul(g, NULL, 0);
+	uint64_t cap = (uint64_t)d->ncu * (per_cu ? per_cu : 4);
 	if (tiles > cap)
 		tiles = cap;
 	return tiles ? (unsigned)tiles : 1;
+}
+
+/* classify launches on the device's own stream (every classify of a device
+ * is serialised there), ordered after and before @user (a caller's stream,
+ * or NULL). */
+static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs *a0,
+			void *user, int iters)
+{
+	int err = 0;
+	struct xfg_kargs a = *a0;
+	unsigned grid = grid_for(d, &a);
+	if (user && user != (void *)d->stream) {
+		HIPCHK(hipEventRecord(d->ev_user, (hipStream_t)user));
+		HIPCHK(hipStreamWaitEvent(d->stream, d->ev_user, 0));
+	}
+	for (int i = 0; i < iters; i++) {
+		if ((err = xfg_launch_classify(ctx->prog_features, &a, grid, d->stream)))
+			goto fail;
+	}
+	if (user && user != (void *)d->stream) {
+		HIPCHK(hipEventRecord(d->ev_done, d->stream));
+		HIPCHK(hipStreamWaitEvent((hipStream_t)user, d->ev_done, 0));
+	}
+	return 0;
+fail:
+	return err;
 }
 
 static int check_batch(xfg_ctx *ctx, int dev, const struct xfg_batch *b, const void *verdicts)
@@ -869,8 +975,7 @@ int xfg_classify(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verd
 	pthread_mutex_unlock(&ctx->lock);
 	err = hip_err(hipSetDevice(d->ordinal));
 	if (!err)
-		err = xfg_launch_classify(ctx->prog_features, &a, grid_for(d, b->count),
-					  stream ? stream : (void *)d->stream);
+		err = launch_batch(ctx, d, &a, stream, 1);
 	return err;
 }
 
@@ -889,14 +994,10 @@ int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t
 	ctx->reduced = 0;
 	fill_kargs(ctx, d, b, verdicts, &a);
 	pthread_mutex_unlock(&ctx->lock);
-	unsigned grid = grid_for(d, b->count);
 	HIPCHK(hipSetDevice(d->ordinal));
 	HIPCHK(hipEventRecord(d->ev0, d->stream));
-	for (int i = 0; i < iters; i++) {
-		err = xfg_launch_classify(ctx->prog_features, &a, grid, d->stream);
-		if (err)
-			goto fail;
-	}
+	if ((err = launch_batch(ctx, d, &a, NULL, iters)))
+		goto fail;
 	HIPCHK(hipEventRecord(d->ev1, d->stream));
 	HIPCHK(hipEventSynchronize(d->ev1));
 	HIPCHK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
@@ -992,7 +1093,9 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t 
 		ctx->reduced = 0;
 		fill_kargs(ctx, d, &sub, dv[k], &a);
 		pthread_mutex_unlock(&ctx->lock);
-		if ((err = xfg_launch_classify(ctx->prog_features, &a, grid_for(d, m), st[k])))
+		/* copies on st[k]; the kernels on the device stream (launch_batch
+		 * orders it after st[k]'s uploads and st[k] after the kernels) */
+		if ((err = launch_batch(ctx, d, &a, st[k], 1)))
 			goto fail;
 		HIPCHK(hipMemcpyAsync(verdicts + c, dv[k], m, hipMemcpyDeviceToHost, st[k]));
 		HIPCHK(hipEventRecord(done[k], st[k]));

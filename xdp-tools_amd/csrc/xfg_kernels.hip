@@ -92,6 +92,29 @@ struct Pkt {
 		uint32_t r = raw16(o);
 		return ((r & 0xff) << 8) | (r >> 8);
 	}
+	// Dword k of the window (k < W / 4).
+	__device__ __forceinline__ uint32_t dw(int k) const { return row[k]; }
+};
+
+// Lookup keys read lazily from a packet view (header bytes still staged).
+template <class P>
+struct LazyKeys {
+	const P &p;
+	__device__ __forceinline__ void eth(uint32_t o, uint32_t &lo, uint32_t &hi) const
+	{
+		lo = p.u32(o);
+		hi = p.raw16(o + 4);
+	}
+	__device__ __forceinline__ void v6(uint32_t o, uint32_t (&k)[4]) const
+	{
+		k[0] = p.u32(o);
+		k[1] = p.u32(o + 4);
+		k[2] = p.u32(o + 8);
+		k[3] = p.u32(o + 12);
+	}
+	__device__ __forceinline__ void v6_dst(uint32_t o6, uint32_t (&k)[4]) const { v6(o6 + 24, k); }
+	__device__ __forceinline__ void v6_src(uint32_t o6, uint32_t (&k)[4]) const { v6(o6 + 8, k); }
+	__device__ __forceinline__ void nd_tgt(uint32_t ond, uint32_t (&k)[4]) const { v6(ond, k); }
 };
 
 // ---------------------------------------------------------------- parse result
@@ -112,8 +135,69 @@ struct Parsed {
 	uint32_t pdst, psrc;   // raw be16 port keys
 };
 
-template <uint32_t FEAT, int W>
-__device__ __forceinline__ Parsed parse(const Pkt<W> &p)
+// Fast path for the dominant, well-formed shapes, read at static offsets
+// from the LDS row: untagged IPv4 with ihl 5 (UDP, TCP or other protocol)
+// and untagged IPv6/UDP without extension headers, each at least as long
+// as every field read here.  It produces exactly what parse_generic()
+// produces for such a packet (same bounds checks, same keys); every other
+// packet takes the generic walk.
+template <uint32_t FEAT, int W, class P>
+__device__ __forceinline__ bool parse_fast(const P &p, Parsed &r)
+{
+	if constexpr (W < 64 || (FEAT & (F_IPV4 | F_IPV6 | F_TCP | F_UDP)) == 0) {
+		return false;
+	} else {
+		const uint32_t len = p.len;
+		const uint32_t d3 = p.dw(3);                 // bytes 12..15
+		const uint32_t et = d3 & 0xffff;              // raw ethertype
+		if (et == 0x0008 && ((d3 >> 16) & 0xff) == 0x45 && len >= 54) {
+			// IPv4, ihl 5: l4 at 34; 54 bytes cover the UDP or TCP header
+			const uint32_t d5 = p.dw(5), d6 = p.dw(6), d7 = p.dw(7), d8 = p.dw(8),
+				       d9 = p.dw(9);
+			const uint32_t proto = d5 >> 24;          // byte 23
+			r.l3 = 1;
+			r.k4a = __builtin_amdgcn_alignbyte(d8, d7, 2);   // daddr 30..33
+			r.k4b = __builtin_amdgcn_alignbyte(d7, d6, 2);   // saddr 26..29
+			r.psrc = d8 >> 16;                        // bytes 34,35
+			r.pdst = d9 & 0xffff;                     // bytes 36,37
+			if ((FEAT & F_UDP) && proto == 17) {
+				const uint32_t ulen = ((d9 >> 8) & 0xff00) | (d9 >> 24);   // be16 38,39
+				if (ulen < 8)
+					r.abort_at = ST_L4;
+				else
+					r.l4proto = 17;
+			} else if ((FEAT & F_TCP) && proto == 6) {
+				const uint32_t doff = (p.dw(11) >> 20) & 0xf;   // byte 46 >> 4
+				if (34 + doff * 4 > len)
+					r.abort_at = ST_L4;
+				else
+					r.l4proto = 6;
+			}
+			return true;
+		}
+		if (et == 0xdd86 && len >= 62 && (p.dw(5) & 0xff) == 17) {
+			// IPv6, next header UDP: l4 at 54 (the 2-byte extension-walk
+			// read at 54 is covered by len >= 62)
+			r.l3 = 3;
+			r.o6 = 14;
+			if constexpr ((FEAT & F_UDP) != 0) {
+				const uint32_t d13 = p.dw(13), d14 = p.dw(14);
+				const uint32_t ulen = ((d14 >> 8) & 0xff00) | (d14 >> 24);   // 58,59
+				r.psrc = d13 >> 16;                   // 54,55
+				r.pdst = d14 & 0xffff;                // 56,57
+				if (ulen < 8)
+					r.abort_at = ST_L4;
+				else
+					r.l4proto = 17;
+			}
+			return true;
+		}
+		return false;
+	}
+}
+
+template <uint32_t FEAT, int W, class P>
+__device__ __forceinline__ Parsed parse(const P &p)
 {
 	Parsed r;
 	r.abort_at = NST;
@@ -124,6 +208,12 @@ __device__ __forceinline__ Parsed parse(const Pkt<W> &p)
 	r.k4a = r.k4b = 0;
 	r.o6 = r.ond = 0;
 	r.pdst = r.psrc = 0;
+	if (parse_fast<FEAT, W, P>(p, r))
+		return r;
+#ifdef XFG_EXP_NO_GENERIC
+	r.abort_at = ST_ETH;
+	return r;
+#endif
 	const uint32_t len = p.len;
 
 	// parse_ethhdr (parsing_helpers.h:100-134), VLAN_MAX_DEPTH 4
@@ -283,14 +373,24 @@ struct Line {
 	__device__ __forceinline__ bool overflow() const { return q3.w & XFG_META_OVERFLOW; }
 };
 
+// NT: non-temporal loads, so random bucket lines do not push the Bloom
+// filter out of L2.
+template <bool NT>
 __device__ __forceinline__ Line load_line(const xfg_tdesc &t, uint32_t b)
 {
 	const u32x4 *p = reinterpret_cast<const u32x4 *>(bucket_ptr(t, b));
 	Line l;
-	l.q0 = p[0];
-	l.q1 = p[1];
-	l.q2 = p[2];
-	l.q3 = p[3];
+	if constexpr (NT) {
+		l.q0 = __builtin_nontemporal_load(p);
+		l.q1 = __builtin_nontemporal_load(p + 1);
+		l.q2 = __builtin_nontemporal_load(p + 2);
+		l.q3 = __builtin_nontemporal_load(p + 3);
+	} else {
+		l.q0 = p[0];
+		l.q1 = p[1];
+		l.q2 = p[2];
+		l.q3 = p[3];
+	}
 	return l;
 }
 
@@ -356,13 +456,13 @@ __device__ __forceinline__ Hit zero_hit(const xfg_tdesc &t)
 }
 
 // Continue a probe past a full home bucket (rare): linear over buckets.
-template <int KIND>
+template <int KIND, bool NT>
 __device__ __forceinline__ Hit probe_chain(const xfg_tdesc &t, uint32_t b, uint32_t k0, uint32_t k1,
 					uint32_t k2, uint32_t k3)
 {
 	for (uint32_t d = 1; d <= t.max_disp; d++) {
 		b = b + 1 == t.nbuckets ? 0 : b + 1;
-		const Line l = load_line(t, b);
+		const Line l = load_line<NT>(t, b);
 		const int i = match<KIND>(l, k0, k1, k2, k3);
 		if (i >= 0)
 			return { (int64_t)b * slots_of<KIND>() + i, l.flag(i) };
@@ -376,7 +476,7 @@ __device__ __forceinline__ Hit probe_chain(const xfg_tdesc &t, uint32_t b, uint3
 // all keys of a stage are loaded together (8 bytes each, L2-resident); the
 // bucket line is fetched only for a key the filter passes, one at a time,
 // which keeps a single 64-byte line live per lane.
-template <int KIND>
+template <int KIND, bool NT = false>
 struct Probe {
 	uint32_t k0, k1, k2, k3;
 	uint32_t b;
@@ -407,50 +507,58 @@ struct Probe {
 			return zero_hit(t);
 		if (!live)
 			return { -1, 0 };
-		const Line l = load_line(t, b);
+		const Line l = load_line<NT>(t, b);
 		const int i = match<KIND>(l, k0, k1, k2, k3);
 		if (i >= 0)
 			return { (int64_t)b * slots_of<KIND>() + i, l.flag(i) };
 		if (l.overflow() && t.max_disp)
-			return probe_chain<KIND>(t, b, k0, k1, k2, k3);
+			return probe_chain<KIND, NT>(t, b, k0, k1, k2, k3);
 		return { -1, 0 };
 	}
 };
 
-// Counter identity of a hit: map id in the top two bits, slot below
-// (slots < 2^30 for every capacity the host accepts).
+// Counter identity of a hit: its index in the global counter space (v4
+// slots, v6 slots, eth slots, ports; xfg_kargs.gbase), CT_NONE for none.
 constexpr uint32_t CT_NONE = 0xffffffffu;
-constexpr uint32_t CT_V4 = 0u << 30, CT_V6 = 1u << 30, CT_ETH = 2u << 30, CT_PORT = 3u << 30;
 
-__device__ __forceinline__ unsigned long long *counter_ptr(const xfg_kargs &a, uint32_t tag)
+// Counter of global index g (threshold compares: no dynamic index into the
+// kernel-argument struct, which would put it in scratch).
+__device__ __forceinline__ unsigned long long *global_counter(const xfg_kargs &a, uint32_t g)
 {
-	const uint32_t slot = tag & 0x3fffffffu;
-	switch (tag >> 30) {
-	case 0: return a.t4.hits + slot;
-	case 1: return a.t6.hits + slot;
-	case 2: return a.te.hits + slot;
-	default: return a.port_hits + slot;
-	}
+	if (g >= a.gbase[3])
+		return a.port_hits + (g - a.gbase[3]);
+	if (g >= a.gbase[2])
+		return a.te.hits + (g - a.gbase[2]);
+	if (g >= a.gbase[1])
+		return a.t6.hits + (g - a.gbase[1]);
+	return a.t4.hits + g;
 }
 
 // CHECK_MAP (xdp-filter/xdpfilt_prog.h:56-64): hit iff the key exists and
 // (value & mask) == mask; the counter bump is deferred to the caller.
-__device__ __forceinline__ bool take(const Hit &h, uint32_t mask, uint32_t ct, uint32_t &tag)
+__device__ __forceinline__ bool take(const Hit &h, uint32_t mask, uint32_t base, uint32_t &tag)
 {
 	if (h.slot >= 0 && (h.flags & mask) == mask) {
-		tag = ct | (uint32_t)h.slot;
+		tag = base + (uint32_t)h.slot;
 		return true;
 	}
 	return false;
 }
 
+// A lookup with mask m can only hit if some key of the map carries every bit
+// of m (the host keeps fmask = OR of all flag bytes): otherwise it is skipped.
+__device__ __forceinline__ bool can_hit(uint32_t fmask, uint32_t m)
+{
+	return (fmask & m) == m;
+}
+
 __device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s_pbits,
 					   uint32_t key, uint32_t mask, uint32_t &tag)
 {
-	if (!((s_pbits[key >> 5] >> (key & 31)) & 1))
+	if (!can_hit(a.port_fmask, mask) || !((s_pbits[key >> 5] >> (key & 31)) & 1))
 		return false;
 	if ((a.port_flags[key] & mask) == mask) {
-		tag = CT_PORT | key;
+		tag = a.gbase[3] + key;
 		return true;
 	}
 	return false;
@@ -459,8 +567,8 @@ __device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s
 // ---------------------------------------------------------------- the program
 // Ordered lookups over a parsed packet; returns the xdp action and sets tag
 // to the first matching rule's counter identity (CT_NONE if none).
-template <uint32_t FEAT, int W>
-__device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p, const Parsed &r,
+template <uint32_t FEAT, bool NT, class KS>
+__device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, const Parsed &r,
 					    const uint32_t *s_pbits, uint32_t &tag)
 {
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;   // VERDICT_HIT
@@ -472,11 +580,14 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 	// lookup_verdict_ethernet (xdpfilt_prog.h:187-196): dst then src
 	if constexpr ((FEAT & F_ETH) != 0) {
 		if (a.te.count) {
-			Probe<2> d, s;
-			d.start(a.te, true, p.u32(0), p.raw16(4));
-			s.start(a.te, true, p.u32(6), p.raw16(10));
-			if (take(d.result(a.te), M_DST, CT_ETH, tag) ||
-			    take(s.result(a.te), M_SRC, CT_ETH, tag))
+			Probe<2, NT> d, s;
+			uint32_t dl, dh, sl, sh;
+			ks.eth(0, dl, dh);
+			ks.eth(6, sl, sh);
+			d.start(a.te, can_hit(a.te.fmask, M_DST), dl, dh);
+			s.start(a.te, can_hit(a.te.fmask, M_SRC), sl, sh);
+			if (take(d.result(a.te), M_DST, a.gbase[2], tag) ||
+			    take(s.result(a.te), M_SRC, a.gbase[2], tag))
 				return HIT;
 		}
 	}
@@ -489,25 +600,30 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 			// ARP:  sip (k4a, SRC); op 1: tip DST; op 2: tip SRC  (:241-261)
 			const bool arp = r.l3 == 2;
 			const bool want_b = !arp || r.arp_op == 1 || r.arp_op == 2;
-			Probe<4> x, y;
-			x.start(a.t4, true, r.k4a);
-			y.start(a.t4, want_b, r.k4b);
+			// The second key's Bloom word is read only when the first key
+			// missed: random L2 requests, not latency, bound this stage.
+			Probe<4, NT> x, y;
 			const uint32_t mx = arp ? M_SRC : M_DST;
 			const uint32_t my = arp ? (r.arp_op == 1 ? M_DST : M_SRC) : M_SRC;
-			if (take(x.result(a.t4), mx, CT_V4, tag) ||
-			    (want_b && take(y.result(a.t4), my, CT_V4, tag)))
+			x.start(a.t4, can_hit(a.t4.fmask, mx), r.k4a);
+			if (take(x.result(a.t4), mx, a.gbase[0], tag))
+				return HIT;
+			y.start(a.t4, want_b && can_hit(a.t4.fmask, my), r.k4b);
+			if (want_b && take(y.result(a.t4), my, a.gbase[0], tag))
 				return HIT;
 		}
 	}
 	if constexpr ((FEAT & F_IPV6) != 0) {
 		if (a.t6.count && r.l3 == 3) {
 			// lookup_verdict_ipv6: dst then src (xdpfilt_prog.h:152-165)
-			const uint32_t o = r.o6;
-			Probe<6> d, s;
-			d.start(a.t6, true, p.u32(o + 24), p.u32(o + 28), p.u32(o + 32), p.u32(o + 36));
-			s.start(a.t6, true, p.u32(o + 8), p.u32(o + 12), p.u32(o + 16), p.u32(o + 20));
-			if (take(d.result(a.t6), M_DST, CT_V6, tag) ||
-			    take(s.result(a.t6), M_SRC, CT_V6, tag))
+			Probe<6, NT> d, s;
+			uint32_t kd[4], kq[4];
+			ks.v6_dst(r.o6, kd);
+			ks.v6_src(r.o6, kq);
+			d.start(a.t6, can_hit(a.t6.fmask, M_DST), kd[0], kd[1], kd[2], kd[3]);
+			s.start(a.t6, can_hit(a.t6.fmask, M_SRC), kq[0], kq[1], kq[2], kq[3]);
+			if (take(d.result(a.t6), M_DST, a.gbase[1], tag) ||
+			    take(s.result(a.t6), M_SRC, a.gbase[1], tag))
 				return HIT;
 		}
 	}
@@ -516,10 +632,12 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 	if constexpr ((FEAT & F_IPV6) != 0) {
 		if (a.t6.count && r.nd) {
 			// NDISC target: NS => DST, NA => SRC (xdpfilt_prog.h:277-285)
-			const uint32_t o = r.ond;
-			Probe<6> t;
-			t.start(a.t6, true, p.u32(o), p.u32(o + 4), p.u32(o + 8), p.u32(o + 12));
-			if (take(t.result(a.t6), r.nd == 135 ? M_DST : M_SRC, CT_V6, tag))
+			const uint32_t mt = r.nd == 135 ? M_DST : M_SRC;
+			Probe<6, NT> t;
+			uint32_t kt[4];
+			ks.nd_tgt(r.ond, kt);
+			t.start(a.t6, can_hit(a.t6.fmask, mt), kt[0], kt[1], kt[2], kt[3]);
+			if (take(t.result(a.t6), mt, a.gbase[1], tag))
 				return HIT;
 		}
 	}
@@ -541,31 +659,25 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const Pkt<W> &p,
 // A rule hit by many packets (a hot port, an attacked address) is summed
 // here and reaches memory once per workgroup; a slot already owned by a
 // different counter sends the bump straight to its global atomic.
-constexpr int CC_ENTRIES = 1024;
+constexpr int CC_ENTRIES = 512;
 
-__device__ __forceinline__ void count_hit(const xfg_kargs &a, uint32_t *s_ctag, uint32_t *s_ccnt,
-					  uint32_t tag, uint32_t n)
+// Returns true when the LDS cache absorbed the n bumps of counter `tag`.
+__device__ __forceinline__ bool cache_hit(uint32_t *s_ctag, uint32_t *s_ccnt, uint32_t tag,
+					  uint32_t n)
 {
-	const uint32_t e = (tag * 0x9E3779B1u) >> 22;   // 10 bits
+	const uint32_t e = (tag * 0x9E3779B1u) >> 23;   // 9 bits
 	uint32_t t = s_ctag[e];
 	if (t == CT_NONE) {
 		t = atomicCAS(&s_ctag[e], CT_NONE, tag);
 		if (t == CT_NONE)
 			t = tag;
 	}
-	if (t == tag)
-		atomicAdd(&s_ccnt[e], n);
-	else
-		atomicAdd(counter_ptr(a, tag), (unsigned long long)n);
+	if (t != tag)
+		return false;
+	atomicAdd(&s_ccnt[e], n);
+	return true;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
-{
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1)
-		v += __shfl_xor(v, o);
-	return v;
-}
 
 __device__ __forceinline__ uint32_t load_len(const xfg_kargs &a, uint64_t i)
 {
@@ -579,8 +691,10 @@ __device__ __forceinline__ const uint8_t *pkt_ptr(const xfg_kargs &a, uint64_t i
 }
 
 // ---------------------------------------------------------------- the kernel
-template <uint32_t FEAT, int W>
-__global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
+// V: build variant bits (production = 0 unless measured better):
+//   1 = non-temporal bucket-line loads, 2 = ask the allocator for 5 waves/SIMD
+template <uint32_t FEAT, int W, int V>
+__global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(const xfg_kargs a)
 {
 	constexpr int CPP = W / 16;            // 16-byte chunks per packet window
 	constexpr int ROWDW = Pkt<W>::ROWDW;   // odd dword stride per LDS row
@@ -608,28 +722,45 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 	const bool guarded = a.offsets != nullptr || a.stride < (uint32_t)W;
 
 	const uint64_t ntiles = (a.n + TILE - 1) / TILE;
+	// dense layout (stride == W, no offsets): a tile is one contiguous block
+	// of TILE * W bytes and chunk c of it sits at byte 16 * c
+	const bool dense = !guarded && a.stride == (uint32_t)W;
 	uint64_t tile = blockIdx.x;
 	u32x4 pre[CPP];
 	uint32_t plen = 0;
+	uint32_t c_ab = 0, c_dr = 0, c_pa = 0;
+	unsigned long long b_ab = 0, b_dr = 0, b_pa = 0;
 	auto issue = [&](uint64_t t) {
 		const uint64_t base = t * TILE;
+		if (dense && base + TILE <= a.n) {
+			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + base * W) + tid;
 #pragma unroll
-		for (int it = 0; it < CPP; it++) {
-			const int c = it * TILE + tid;
-			const int pk = c / CPP, sub = c % CPP;
-			const uint64_t gi = base + pk;
-			pre[it] = u32x4{ 0, 0, 0, 0 };
-			if (gi < a.n && (!guarded || (uint32_t)sub * 16 < load_len(a, gi)))
-				pre[it] = __builtin_nontemporal_load(
-					reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16));
+			for (int it = 0; it < CPP; it++)
+				pre[it] = __builtin_nontemporal_load(src + it * TILE);
+		} else {
+#pragma unroll
+			for (int it = 0; it < CPP; it++) {
+				const int c = it * TILE + tid;
+				const int pk = c / CPP, sub = c % CPP;
+				const uint64_t gi = base + pk;
+				pre[it] = u32x4{ 0, 0, 0, 0 };
+				if (gi < a.n && (!guarded || (uint32_t)sub * 16 < load_len(a, gi)))
+					pre[it] = __builtin_nontemporal_load(
+						reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16));
+			}
 		}
 		plen = base + tid < a.n ? load_len(a, base + tid) : 0;
 	};
+#ifndef XFG_EXP_NO_PREFETCH
 	if (tile < ntiles)
 		issue(tile);
+#endif
 
 	for (; tile < ntiles; tile += gridDim.x) {
 		const uint64_t base = tile * TILE;
+#ifdef XFG_EXP_NO_PREFETCH
+		issue(tile);
+#endif
 		// 1. stage the prefetched windows into LDS
 #pragma unroll
 		for (int it = 0; it < CPP; it++) {
@@ -643,8 +774,10 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 		}
 		const uint32_t len = plen;
 		__syncthreads();
+#ifndef XFG_EXP_NO_PREFETCH
 		if (tile + gridDim.x < ntiles)
 			issue(tile + gridDim.x);   // next tile's stream overlaps this tile's work
+#endif
 
 		// 2-4. parse, match, verdict
 		const uint64_t gi = base + tid;
@@ -656,7 +789,7 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 				act = p.u8(0) & 1;
 			} else {
 				const Parsed r = parse<FEAT, W>(p);
-				act = lookups<FEAT, W>(a, p, r, s_pbits, tag);
+				act = lookups<FEAT, (V & 1) != 0>(a, LazyKeys<Pkt<W>>{ p }, r, s_pbits, tag);
 			}
 			a.verdicts[gi] = (uint8_t)act;
 		}
@@ -664,50 +797,448 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 			tag = CT_NONE;
 
 		// counter bump: lanes of the wave hitting the same rule are merged
-		// (two leader rounds), then summed in the LDS counter cache
-#pragma unroll 1
-		for (int rnd = 0; rnd < 2; rnd++) {
+		// (one leader round), then summed in the LDS counter cache; a bump
+		// the cache cannot take goes straight to a memory-side atomic
+		{
 			const unsigned long long pend = __ballot(tag != CT_NONE);
-			if (!pend)
-				break;
-			const int leader = __ffsll((long long)pend) - 1;
-			const uint32_t lt = __shfl(tag, leader);
-			const bool mine = tag == lt;
-			const unsigned long long same = __ballot(mine);
-			if (lane == leader)
-				count_hit(a, s_ctag, s_ccnt, lt, (uint32_t)__popcll(same));
-			if (mine)
-				tag = CT_NONE;
-		}
-		if (tag != CT_NONE)
-			count_hit(a, s_ctag, s_ccnt, tag, 1);
-
-		// 5. per-action stats (xdp_stats_record_action)
-#pragma unroll
-		for (uint32_t k = 0; k < 3; k++) {
-			const unsigned long long m = __ballot(act == k);
-			const uint32_t bytes = wave_sum(act == k ? len : 0);
-			if (lane == 0 && m) {
-				atomicAdd(&s_stats[2 * k], (unsigned long long)__popcll(m));
-				atomicAdd(&s_stats[2 * k + 1], (unsigned long long)bytes);
+			if (pend) {
+				const int leader = __ffsll((long long)pend) - 1;
+				const uint32_t lt = __shfl(tag, leader);
+				const bool mine = tag == lt;
+				const unsigned long long same = __ballot(mine);
+				if (lane == leader) {
+					const uint32_t cnt = (uint32_t)__popcll(same);
+					if (!cache_hit(s_ctag, s_ccnt, lt, cnt))
+						atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
+				}
+				if (mine)
+					tag = CT_NONE;
 			}
+		}
+		if (tag != CT_NONE && !cache_hit(s_ctag, s_ccnt, tag, 1))
+			atomicAdd(global_counter(a, tag), 1ull);
+
+		// 5. per-action stats (xdp_stats_record_action), kept per lane
+#ifdef XFG_EXP_NO_STATS
+		if (0) {
+#else
+		if (act == A_ABORTED) {
+#endif
+			c_ab++;
+			b_ab += len;
+		} else if (act == A_DROP) {
+			c_dr++;
+			b_dr += len;
+		} else if (act == A_PASS) {
+			c_pa++;
+			b_pa += len;
 		}
 		__syncthreads();   // LDS window reuse
 	}
+	// per-action stats: lane sums -> wave sums -> workgroup (LDS) -> device
+	{
+		unsigned long long v[6] = { c_ab, b_ab, c_dr, b_dr, c_pa, b_pa };
+#pragma unroll
+		for (int k = 0; k < 6; k++) {
+			unsigned long long x = v[k];
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1)
+				x += __shfl_xor(x, o);
+			if (lane == 0 && x)
+				atomicAdd(&s_stats[k], x);
+		}
+	}
+	__syncthreads();
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
 	for (int i = tid; i < CC_ENTRIES; i += TILE)
 		if (s_ctag[i] != CT_NONE && s_ccnt[i])
-			atomicAdd(counter_ptr(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
+			atomicAdd(global_counter(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
+}
+
+// ---------------------------------------------------------------- streamed kernel
+// The fixed-stride layout (stride >= 64, 16-byte aligned) with the header
+// stream taken off the lookup waves.  A workgroup is four lookup waves (one
+// packet per lane) plus one I/O wave:
+//
+//   I/O wave      global_load_lds (LDS-DMA, no VGPRs) of tile k+2's header
+//                 windows and lengths into the buffer tile k has just
+//                 released; then the counter atomics and the verdict store
+//                 of tile k-1, read from LDS;
+//   lookup waves  parse tile k from LDS, copy its keys to registers, release
+//                 the buffer (barrier P), probe, and leave verdict bytes and
+//                 cold counter bumps in LDS (barrier E).
+//
+// A wave's vector-memory counter completes in issue order, so a lookup wave
+// that also streamed headers or issued atomics would wait for them at every
+// probe; here its counter holds nothing but its own probes.
+//
+// Tile buffer: 256 windows of 64 bytes, 16-byte chunk c of packet p at chunk
+// slot p*4 + (c ^ ((p >> 2) & 3)): every LDS-DMA instruction writes 1 KiB
+// lane-linearly (the swizzle is applied to the source address), and a lane-
+// per-packet read of any dword touches 16 distinct banks per 16 lanes.
+constexpr int IO_THREADS = TILE + 64;
+constexpr int SBUF_DW = TILE * 16;   // one tile buffer, dwords
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
+{
+	return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// 16 bytes per lane from gsrc to LDS lds + 16 * lane (lds wave-uniform).  The
+// compiler does not see this load: its completion is counted by hand.
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds)
+{
+	unsigned keep;
+	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+		     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+		     : "=&s"(keep)
+		     : "v"(gsrc), "s"(lds)
+		     : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm()
+{
+	asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Workgroup barrier that waits for this wave's LDS operations only (an LDS-
+// DMA in flight stays in flight; __syncthreads() would drain it).
+__device__ __forceinline__ void wg_barrier()
+{
+	asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Packet view over a swizzled tile buffer (same interface as Pkt<64>).
+struct SPkt {
+	const uint32_t *tb;   // tile buffer
+	uint32_t base;        // 16 * p
+	uint32_t xr;          // (p >> 2) & 3
+	const uint8_t *g;
+	uint32_t len;
+
+	__device__ __forceinline__ uint32_t dw(uint32_t k) const
+	{
+		return tb[base + (((k >> 2) ^ xr) << 2) + (k & 3)];
+	}
+	__device__ __forceinline__ uint32_t u8(uint32_t o) const
+	{
+		if (o < 64)
+			return (dw(o >> 2) >> (8 * (o & 3))) & 0xff;
+		return g[o];
+	}
+	__device__ __forceinline__ uint32_t u32(uint32_t o) const
+	{
+		if (o + 4 <= 64) {
+			const uint32_t k = o >> 2;
+			return __builtin_amdgcn_alignbyte(dw(k < 15 ? k + 1 : 15), dw(k), o & 3);
+		}
+		return g[o] | (g[o + 1] << 8) | (g[o + 2] << 16) | ((uint32_t)g[o + 3] << 24);
+	}
+	__device__ __forceinline__ uint32_t raw16(uint32_t o) const
+	{
+		if (o + 2 <= 64) {
+			const uint32_t k = o >> 2;
+			return __builtin_amdgcn_alignbyte(dw(k < 15 ? k + 1 : 15), dw(k), o & 3) & 0xffffu;
+		}
+		return g[o] | ((uint32_t)g[o + 1] << 8);
+	}
+	__device__ __forceinline__ uint32_t be16(uint32_t o) const
+	{
+		uint32_t r = raw16(o);
+		return ((r & 0xff) << 8) | (r >> 8);
+	}
+};
+
+// Lookup keys copied to registers before the tile buffer is released; the
+// NDISC target (rare) is read from the packet in HBM.
+struct RegKeys {
+	uint32_t e0, e1, e2;          // bytes 0..11: dst MAC, src MAC
+	uint32_t d6[4], s6[4];        // IPv6 daddr, saddr
+	const uint8_t *g;
+
+	__device__ __forceinline__ void eth(uint32_t o, uint32_t &lo, uint32_t &hi) const
+	{
+		if (o == 0) {
+			lo = e0;
+			hi = e1 & 0xffff;
+		} else {
+			lo = __builtin_amdgcn_alignbyte(e2, e1, 2);
+			hi = e2 >> 16;
+		}
+	}
+	__device__ __forceinline__ void v6_dst(uint32_t, uint32_t (&k)[4]) const
+	{
+		k[0] = d6[0]; k[1] = d6[1]; k[2] = d6[2]; k[3] = d6[3];
+	}
+	__device__ __forceinline__ void v6_src(uint32_t, uint32_t (&k)[4]) const
+	{
+		k[0] = s6[0]; k[1] = s6[1]; k[2] = s6[2]; k[3] = s6[3];
+	}
+	__device__ __forceinline__ void nd_tgt(uint32_t o, uint32_t (&k)[4]) const
+	{
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const uint8_t *q = g + o + 4 * i;
+			k[i] = q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24);
+		}
+	}
+};
+
+template <uint32_t FEAT, int V>
+__global__ __launch_bounds__(IO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void xfg_classify_stream_kernel(const xfg_kargs a)
+{
+	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
+	__shared__ __attribute__((aligned(16))) uint32_t ring[2 * SBUF_DW];
+	__shared__ __attribute__((aligned(16))) uint32_t s_lens[2][TILE];
+	__shared__ uint32_t s_verd[2][TILE / 4];
+	__shared__ uint32_t s_q[2][TILE];
+	__shared__ uint32_t s_qn[2];
+	__shared__ uint32_t s_pbits[PORTS ? 2048 : 1];
+	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
+	__shared__ unsigned long long s_stats[6];
+
+	const int tid = threadIdx.x;
+	const int lane = tid & 63;
+	const bool io = tid >= TILE;
+	if (tid < 6)
+		s_stats[tid] = 0;
+	if (tid < 2)
+		s_qn[tid] = 0;
+	for (int i = tid; i < CC_ENTRIES; i += IO_THREADS) {
+		s_ctag[i] = CT_NONE;
+		s_ccnt[i] = 0;
+	}
+	if constexpr (PORTS) {
+		if (a.port_count)
+			for (int i = tid; i < 2048; i += IO_THREADS)
+				s_pbits[i] = a.port_bits[i];
+	}
+
+	const uint64_t ntiles = (a.n + TILE - 1) / TILE;
+	const uint64_t G = gridDim.x;
+	const uint64_t b = blockIdx.x;
+	const uint64_t K = b < ntiles ? (ntiles - 1 - b) / G + 1 : 0;
+	const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+	const uint32_t lens_lds = __builtin_amdgcn_readfirstlane(lds_addr(&s_lens[0][0]));
+	const uint32_t esz = a.lens_u16 ? 2 : 4;
+
+	// I/O wave: 17 LDS-DMA instructions per tile (16 window KiBs + lengths)
+	auto io_issue = [&](uint64_t k) {
+		const uint64_t p0 = (b + k * G) * TILE;
+		const uint32_t buf = (uint32_t)(k & 1);
+#pragma unroll
+		for (int j = 0; j < 16; j++) {
+			const uint32_t s = j * 64 + lane;
+			const uint32_t p = s >> 2;
+			const uint32_t c = (s & 3) ^ ((p >> 2) & 3);
+			const uint64_t gi = p0 + p;
+			const uint8_t *src = gi < a.n ? a.data + gi * a.stride + c * 16 : a.data;
+			glds16(src, ring_lds + buf * (SBUF_DW * 4) + j * 1024);
+		}
+		const uint64_t first = p0 + (uint64_t)lane * (16 / esz);
+		const uint8_t *lsrc = static_cast<const uint8_t *>(a.lens);
+		if (lane < (a.lens_u16 ? 32 : 64))
+			glds16(first < a.n ? lsrc + first * esz : lsrc, lens_lds + buf * (TILE * 4));
+	};
+	// I/O wave: counter atomics and verdict bytes of tile k (LDS parity k & 1)
+	auto io_flush = [&](uint64_t k) {
+		const uint32_t q = (uint32_t)(k & 1);
+		const uint32_t nq = s_qn[q];
+		if (!(a.ablate & 2))
+			for (uint32_t i = lane; i < nq; i += 64)
+				atomicAdd(global_counter(a, s_q[q][i]), 1ull);
+		const uint64_t p0 = (b + k * G) * TILE;
+		const uint32_t v = s_verd[q][lane];
+		if (p0 + TILE <= a.n && !((uintptr_t)a.verdicts & 3)) {
+			reinterpret_cast<uint32_t *>(a.verdicts + p0)[lane] = v;
+		} else {
+#pragma unroll
+			for (int i = 0; i < 4; i++)
+				if (p0 + lane * 4 + i < a.n)
+					a.verdicts[p0 + lane * 4 + i] = (uint8_t)(v >> (8 * i));
+		}
+		if (lane == 0)
+			s_qn[q] = 0;
+	};
+
+	uint32_t c_ab = 0, c_dr = 0, c_pa = 0;
+	unsigned long long b_ab = 0, b_dr = 0, b_pa = 0;
+
+	if (io) {
+		if (K > 0)
+			io_issue(0);
+		if (K > 1) {
+			io_issue(1);
+			wait_vm<17>();
+		} else {
+			wait_vm<0>();
+		}
+	}
+	wg_barrier();   // S: LDS set up, tile 0 landed
+
+	for (uint64_t k = 0; k < K; k++) {
+		const uint32_t par = (uint32_t)(k & 1);
+		if (io) {
+			wg_barrier();   // P_k: tile k parsed, its buffer free
+			if (k + 2 < K) {
+				io_issue(k + 2);
+				if (k >= 1)
+					io_flush(k - 1);
+				wait_vm<17>();   // tile k+1 (and the flush before it) landed
+			} else {
+				if (k >= 1)
+					io_flush(k - 1);
+				wait_vm<0>();
+			}
+			wg_barrier();   // E_k
+			continue;
+		}
+		// lookup waves
+		const uint64_t gi = (b + k * G) * TILE + tid;
+		const bool valid = gi < a.n;
+		const uint32_t len = a.lens_u16 ? reinterpret_cast<const uint16_t *>(s_lens[par])[tid]
+						: s_lens[par][tid];
+		const SPkt p{ ring + par * SBUF_DW, (uint32_t)tid * 16, ((uint32_t)tid >> 2) & 3,
+			      a.data + gi * a.stride, len };
+		Parsed r;
+		RegKeys ks;
+		ks.g = p.g;
+		uint32_t act = A_NONE;
+		if (valid) {
+			if (a.ablate & 4) {
+				act = p.u8(0) & 1;
+			} else {
+				r = parse<FEAT, 64>(p);
+				if constexpr ((FEAT & F_ETH) != 0) {
+					ks.e0 = p.dw(0);
+					ks.e1 = p.dw(1);
+					ks.e2 = p.dw(2);
+				}
+				if constexpr ((FEAT & F_IPV6) != 0) {
+					if (r.l3 == 3) {
+#pragma unroll
+						for (int i = 0; i < 4; i++) {
+							ks.s6[i] = p.u32(r.o6 + 8 + 4 * i);
+							ks.d6[i] = p.u32(r.o6 + 24 + 4 * i);
+						}
+					}
+				}
+			}
+		}
+		wg_barrier();   // P_k
+		uint32_t tag = CT_NONE;
+		if (valid && !(a.ablate & 4))
+			act = lookups<FEAT, (V & 1) != 0>(a, ks, r, s_pbits, tag);
+		reinterpret_cast<uint8_t *>(s_verd[par])[tid] = (uint8_t)act;
+		if (a.ablate & 2)
+			tag = CT_NONE;
+
+		// counter bump: wave leader merge, LDS counter cache, else queue the
+		// bump for the I/O wave
+		bool cold = false;
+		{
+			const unsigned long long pend = __ballot(tag != CT_NONE);
+			if (pend) {
+				const int leader = __ffsll((long long)pend) - 1;
+				const uint32_t lt = __shfl(tag, leader);
+				const bool mine = tag == lt;
+				const unsigned long long same = __ballot(mine);
+				const uint32_t cnt = (uint32_t)__popcll(same);
+				if (lane == leader && !cache_hit(s_ctag, s_ccnt, lt, cnt)) {
+					if (cnt == 1)
+						cold = true;
+					else
+						atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
+				}
+				if (mine && !cold)
+					tag = CT_NONE;
+			}
+		}
+		if (tag != CT_NONE && !cold) {
+			if (cache_hit(s_ctag, s_ccnt, tag, 1))
+				tag = CT_NONE;
+			else
+				cold = true;
+		}
+		{
+			const unsigned long long m = __ballot(cold);
+			if (m) {
+				const int first = __ffsll((long long)m) - 1;
+				uint32_t qb = 0;
+				if (lane == first)
+					qb = atomicAdd(&s_qn[par], (uint32_t)__popcll(m));
+				qb = __shfl(qb, first);
+				if (cold) {
+					const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+						(uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+					s_q[par][qb + rank] = tag;
+				}
+			}
+		}
+
+		if (act == A_ABORTED) {
+			c_ab++;
+			b_ab += len;
+		} else if (act == A_DROP) {
+			c_dr++;
+			b_dr += len;
+		} else if (act == A_PASS) {
+			c_pa++;
+			b_pa += len;
+		}
+		wg_barrier();   // E_k
+	}
+	if (io && K > 0)
+		io_flush(K - 1);
+
+	{
+		unsigned long long v[6] = { c_ab, b_ab, c_dr, b_dr, c_pa, b_pa };
+#pragma unroll
+		for (int k = 0; k < 6; k++) {
+			unsigned long long x = v[k];
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1)
+				x += __shfl_xor(x, o);
+			if (lane == 0 && x)
+				atomicAdd(&s_stats[k], x);
+		}
+	}
+	__syncthreads();
+	if (tid < 6 && s_stats[tid])
+		atomicAdd(&a.stats[tid], s_stats[tid]);
+	for (int i = tid; i < CC_ENTRIES; i += IO_THREADS)
+		if (s_ctag[i] != CT_NONE && s_ccnt[i])
+			atomicAdd(global_counter(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
 }
 
 template <uint32_t FEAT>
 hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 {
-	if (a.window <= 64)
-		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64>), dim3(grid), dim3(TILE), 0, s, a);
-	else
-		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128>), dim3(grid), dim3(TILE), 0, s, a);
+	if (a.streamed) {
+		hipLaunchKernelGGL((xfg_classify_stream_kernel<FEAT, 0>), dim3(grid), dim3(IO_THREADS), 0, s, a);
+	} else if (a.window <= 64) {
+		// build variants of the headline program (diagnostics: XFG_VARIANT)
+		if constexpr (FEAT == (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH | F_DENY)) {
+			switch (a.variant) {
+			case 1:
+				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 1>), dim3(grid), dim3(TILE), 0, s, a);
+				return hipGetLastError();
+			case 2:
+				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 2>), dim3(grid), dim3(TILE), 0, s, a);
+				return hipGetLastError();
+			case 3:
+				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 3>), dim3(grid), dim3(TILE), 0, s, a);
+				return hipGetLastError();
+			default:
+				break;
+			}
+		}
+		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 0>), dim3(grid), dim3(TILE), 0, s, a);
+	} else {
+		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128, 0>), dim3(grid), dim3(TILE), 0, s, a);
+	}
 	return hipGetLastError();
 }
 
@@ -737,6 +1268,38 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 		return -22; /* -EINVAL */
 	}
 	return e == hipSuccess ? 0 : -(int)e - 1000;
+}
+
+// Resident workgroups per CU of the classify kernel a launch would use
+// (grid sizing: one persistent wave of workgroups); window 1 = the streamed
+// kernel.
+template <uint32_t FEAT>
+static int occupancy_feat(uint32_t window)
+{
+	int n = 0;
+	hipError_t e = window == 1
+		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_stream_kernel<FEAT, 0>, IO_THREADS, 0)
+		: window <= 64
+		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_kernel<FEAT, 64, 0>, TILE, 0)
+		: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_kernel<FEAT, 128, 0>, TILE, 0);
+	return e == hipSuccess && n > 0 ? n : 4;
+}
+
+extern "C" int xfg_classify_occupancy(uint32_t prog_features, uint32_t window)
+{
+	switch (prog_features) {
+	case F_UDP | F_DENY:              return occupancy_feat<F_UDP | F_DENY>(window);
+	case F_TCP | F_DENY:              return occupancy_feat<F_TCP | F_DENY>(window);
+	case F_IPV4 | F_IPV6 | F_DENY:    return occupancy_feat<F_IPV4 | F_IPV6 | F_DENY>(window);
+	case F_ETH | F_DENY:              return occupancy_feat<F_ETH | F_DENY>(window);
+	case XFG_ALL | F_DENY:            return occupancy_feat<XFG_ALL | F_DENY>(window);
+	case F_UDP | XFG_ALLOW:           return occupancy_feat<F_UDP | XFG_ALLOW>(window);
+	case F_TCP | XFG_ALLOW:           return occupancy_feat<F_TCP | XFG_ALLOW>(window);
+	case F_IPV4 | F_IPV6 | XFG_ALLOW: return occupancy_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(window);
+	case F_ETH | XFG_ALLOW:           return occupancy_feat<F_ETH | XFG_ALLOW>(window);
+	case XFG_ALL | XFG_ALLOW:         return occupancy_feat<XFG_ALL | XFG_ALLOW>(window);
+	default:                          return 4;
+	}
 }
 
 // Streaming-read probe: the achievable HBM read rate on this device, used by

@@ -72,7 +72,8 @@ struct xfg_tdesc {
 	uint32_t nslots;
 	uint32_t seed;
 	uint32_t bloom_words;        /* 0 => no prefilter */
-	uint32_t pad;
+	uint32_t fmask;              /* OR of every key's flag bits on any device: a
+				      * lookup whose mask is not covered cannot hit */
 };
 
 /* Kernel arguments of one classify launch. */
@@ -93,8 +94,15 @@ struct xfg_kargs {
 	uint8_t *verdicts;
 	uint32_t ablate;              /* diagnostics only (XFG_ABLATE env), 0 in production:
 				       * 2 = no counter atomics, 4 = stage only (no parse) */
-	uint32_t pad;
+	uint32_t variant;             /* diagnostics only (XFG_VARIANT env): build variant */
+	uint32_t port_fmask;          /* OR of the port flag bytes (see tdesc.fmask) */
+	uint32_t streamed;            /* 1: the streamed kernel (I/O wave + lookup waves) */
+	/* Global counter index space (the LDS counter cache's tags): v4 slots,
+	 * v6 slots, eth slots (each with its zero-key slot), then the 65536
+	 * ports; gbase[i] = first index of each. */
+	uint32_t gbase[4];
 };
+
 
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
 #define XFG_HD __host__ __device__ __forceinline__
