@@ -171,7 +171,9 @@ def setup(args, rank, local):
     # ---- traffic: C3 mix, shard seeded by rank
     t0 = time.time()
     data, lens = X.gen_workload(3 + 1000 * rank, 3, n, stride, v4=v4, ports=ports,
-                                dst_permille=500, port_permille=250, bad_permille=10)
+                                dst_permille=getattr(args, "dst_permille", 500),
+                                port_permille=getattr(args, "port_permille", 250),
+                                bad_permille=10)
     lens16 = lens.astype(np.uint16)
     gen_s = time.time() - t0
 

@@ -42,11 +42,13 @@ def main():
             kv = dict(x.split("=") for x in v.split(","))
             variants.append(("env", v, kv))
     res = {str(v[1]): [] for v in variants}
-    knobs = {"XFG_ABLATE", "XFG_VARIANT", "XFG_GRID_PER_CU"}
+    knobs = {"XFG_ABLATE", "XFG_VARIANT", "XFG_GRID_PER_CU", "XFG_KERNEL"}
+    base_env = {k: os.environ[k] for k in knobs if k in os.environ}   # e.g. XFG_VARIANT under rocprof
     for _ in range(a.rounds):
         for kind, key, kv in variants:
             for k in knobs:
                 os.environ.pop(k, None)
+            os.environ.update(base_env)
             if kind == "mask":
                 os.environ["XFG_ABLATE"] = str(key)
             else:

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Instruction-mix PMC passes on the headline classify kernel (diagnostics).
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT="$GRAFT_REPO_ROOT/gpurun_out"; mkdir -p "$OUT"
+TAG=${1:-r01}
+fatal() { [ "$1" -eq 124 ] || [ "$1" -eq 137 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
+cd /tmp && export TMPDIR=/tmp
+i=0
+PM=(${PMC_SETS:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" "SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_BRANCH SQ_WAVES" "SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"})
+for pmc in "${PM[@]}"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $pmc --kernel-trace --output-format csv -d "$OUT/pmc_${TAG}_$i" -o run -- \
+     python3 "$GRAFT_REPO_ROOT/tools/ablate.py" --masks 0 --rounds 1 --iters 2 > "$OUT/pmc_${TAG}_$i.log" 2>&1
+  rc=$?; echo "pmc[$pmc] rc=$rc"; fatal $rc && exit $rc
+done
+python3 "$GRAFT_REPO_ROOT/tools/pmc_summary.py" "$OUT"/pmc_${TAG}_* > "$OUT/pmc_${TAG}.json"
+cat "$OUT/pmc_${TAG}.json"
+exit 0

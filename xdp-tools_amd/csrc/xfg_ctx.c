@@ -56,6 +56,13 @@ struct xfg_dev {
 	unsigned long long *stats;      /* 10 */
 	unsigned long long *red_stats;  /* 10 */
 	void *sink;                     /* stream-read probe sink */
+	unsigned long long *prof;       /* diagnostics: XFG_PROF_WG x 8 phase cycles */
+	/* port table (xfg_layout.h): host mirror of this device's port flag
+	 * bytes, rebuilt into port_tab before a launch when dirty */
+	uint8_t *port_flags_h;
+	uint32_t *port_tab;
+	uint32_t port_tab_disp;
+	int port_tab_ok, port_tab_dirty;
 	int occ64, occ128, occ_st;      /* resident classify workgroups per CU */
 	hipEvent_t ev_user, ev_done;    /* ordering against a caller's stream */
 };
@@ -172,6 +179,9 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->stats);
 	hipFree(d->red_stats);
 	hipFree(d->sink);
+	hipFree(d->prof);
+	hipFree(d->port_tab);
+	free(d->port_flags_h);
 	if (d->ev_user)
 		hipEventDestroy(d->ev_user);
 	if (d->ev_done)
@@ -214,6 +224,15 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	HIPCHK(hipMalloc((void **)&d->stats, 10 * 8));
 	HIPCHK(hipMemset(d->stats, 0, 10 * 8));
 	HIPCHK(hipMalloc(&d->sink, 16 * 65536));
+	HIPCHK(hipMalloc((void **)&d->prof, XFG_PROF_WG * 8 * 8));
+	HIPCHK(hipMalloc((void **)&d->port_tab, XFG_PORT_TAB * 4));
+	d->port_flags_h = calloc(XFG_PORT_MAP_ENTRIES, 1);
+	if (!d->port_flags_h) {
+		err = -ENOMEM;
+		goto fail;
+	}
+	d->port_tab_dirty = 1;
+	HIPCHK(hipMemset(d->prof, 0, XFG_PROF_WG * 8 * 8));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
 	d->occ64 = xfg_classify_occupancy(ctx->prog_features, 64);
@@ -547,6 +566,8 @@ static int port_store(xfg_ctx *ctx, uint32_t k, const uint64_t *vals)
 		uint8_t f = vals[i] & 63;
 		unsigned long long h = vals[i] >> XFG_COUNTER_SHIFT;
 		any |= f;
+		d->port_flags_h[k] = f;
+		d->port_tab_dirty = 1;
 		err = dev_write(d, d->port_flags + k, &f, 1);
 		if (!err)
 			err = dev_write(d, d->port_hits + k, &h, 8);
@@ -842,10 +863,45 @@ out:
 }
 
 /* ------------------------------------------------------------------ classify */
-static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b,
-		       uint8_t *verdicts, struct xfg_kargs *a)
+/* Rebuild a device's LDS port table from its flag bytes (linear probing from
+ * xfg_port_slot()); with more than XFG_PORT_TAB_MAX ruled ports the kernel
+ * uses the bitmap + port_flags path instead. */
+static int port_tab_refresh(struct xfg_dev *d)
+{
+	uint32_t tab[XFG_PORT_TAB];
+	uint32_t n = 0, disp = 0;
+	if (!d->port_tab_dirty)
+		return 0;
+	memset(tab, 0, sizeof(tab));
+	for (uint32_t k = 0; k < XFG_PORT_MAP_ENTRIES; k++) {
+		if (!d->port_flags_h[k])
+			continue;
+		if (++n > XFG_PORT_TAB_MAX)
+			break;
+		uint32_t sl = xfg_port_slot(k), dd = 0;
+		while (tab[sl]) {
+			sl = (sl + 1) & (XFG_PORT_TAB - 1);
+			dd++;
+		}
+		tab[sl] = ((uint32_t)d->port_flags_h[k] << 16) | k;
+		if (dd > disp)
+			disp = dd;
+	}
+	d->port_tab_ok = n <= XFG_PORT_TAB_MAX;
+	d->port_tab_disp = disp;
+	d->port_tab_dirty = 0;
+	if (!d->port_tab_ok)
+		return 0;
+	return dev_write(d, d->port_tab, tab, sizeof(tab));
+}
+
+static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b,
+		      uint8_t *verdicts, struct xfg_kargs *a)
 {
 	memset(a, 0, sizeof(*a));
+	int err = port_tab_refresh(d);
+	if (err)
+		return err;
 	struct xfg_tdesc *td[NMAPS_HASH] = { &a->t4, &a->t6, &a->te };
 	for (int i = 0; i < NMAPS_HASH; i++) {
 		xfg_table_desc(&ctx->t[i], td[i]);
@@ -865,7 +921,10 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 	a->port_bits = d->port_bits;
 	a->port_hits = d->port_hits;
 	a->port_count = ctx->port_count;
+	a->port_tab = d->port_tab_ok ? d->port_tab : NULL;
+	a->port_tab_disp = d->port_tab_disp;
 	a->stats = d->stats;
+	a->prof = d->prof;
 	a->data = b->data;
 	a->offsets = b->offsets;
 	a->lens = b->lens;
@@ -882,8 +941,8 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 	 * byte 64 are read from HBM by the few packets that have them). */
 	a->streamed = !b->offsets && b->stride >= 64 && !((uintptr_t)b->lens & 15);
 	const char *ks = getenv("XFG_KERNEL");    /* diagnostics only */
-	if (ks && !strcmp(ks, "classic"))
-		a->streamed = 0;
+	if (!ks || strcmp(ks, "stream"))
+		a->streamed = 0;   /* experimental: opt-in until it beats the classic kernel */
 	if (a->streamed)
 		a->window = 64;
 	/* Diagnostics only: XFG_ABLATE=<mask> (1 = treat every table as empty,
@@ -900,6 +959,7 @@ static void fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *
 			a->port_count = 0;
 		}
 	}
+	return 0;
 }
 
 /* One persistent wave of workgroups: every resident slot of every CU. */
@@ -971,9 +1031,10 @@ int xfg_classify(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verd
 	struct xfg_kargs a;
 	pthread_mutex_lock(&ctx->lock);
 	ctx->reduced = 0;
-	fill_kargs(ctx, d, b, verdicts, &a);
+	err = fill_kargs(ctx, d, b, verdicts, &a);
 	pthread_mutex_unlock(&ctx->lock);
-	err = hip_err(hipSetDevice(d->ordinal));
+	if (!err)
+		err = hip_err(hipSetDevice(d->ordinal));
 	if (!err)
 		err = launch_batch(ctx, d, &a, stream, 1);
 	return err;
@@ -992,8 +1053,10 @@ int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t
 	float ms = 0;
 	pthread_mutex_lock(&ctx->lock);
 	ctx->reduced = 0;
-	fill_kargs(ctx, d, b, verdicts, &a);
+	err = fill_kargs(ctx, d, b, verdicts, &a);
 	pthread_mutex_unlock(&ctx->lock);
+	if (err)
+		return err;
 	HIPCHK(hipSetDevice(d->ordinal));
 	HIPCHK(hipEventRecord(d->ev0, d->stream));
 	if ((err = launch_batch(ctx, d, &a, NULL, iters)))
@@ -1091,8 +1154,10 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t 
 		struct xfg_kargs a;
 		pthread_mutex_lock(&ctx->lock);
 		ctx->reduced = 0;
-		fill_kargs(ctx, d, &sub, dv[k], &a);
+		err = fill_kargs(ctx, d, &sub, dv[k], &a);
 		pthread_mutex_unlock(&ctx->lock);
+		if (err)
+			goto fail;
 		/* copies on st[k]; the kernels on the device stream (launch_batch
 		 * orders it after st[k]'s uploads and st[k] after the kernels) */
 		if ((err = launch_batch(ctx, d, &a, st[k], 1)))
@@ -1290,5 +1355,21 @@ int xfg_comm_allreduce(xfg_ctx *ctx)
 	ctx->reduced = 1;
 	return 0;
 fail:
+	return err;
+}
+
+/* Diagnostics: the per-workgroup phase cycles of the last profiled launch
+ * (XFG_VARIANT=4), XFG_PROF_WG x 8 u64; the record is zeroed after reading. */
+int xfg_diag_prof(xfg_ctx *ctx, int dev, uint64_t *out, uint64_t n)
+{
+	if (!ctx || !out || dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[dev];
+	uint64_t max = (uint64_t)XFG_PROF_WG * 8;
+	if (n > max)
+		n = max;
+	int err = dev_read(d, out, d->prof, n * 8);
+	if (!err)
+		err = hip_err(hipMemset(d->prof, 0, max * 8));
 	return err;
 }

@@ -45,6 +45,13 @@ constexpr uint32_t F_IPV6 = 1u << 2;
 constexpr uint32_t F_IPV4 = 1u << 3;
 constexpr uint32_t F_ETH = 1u << 4;
 constexpr uint32_t F_DENY = 1u << 6;
+// Diagnostics only (XFG_VARIANT >= 0x100 on the headline program): feature-
+// word bits that remove a code path to measure its instruction cost.
+// Results are wrong with any of them set.
+constexpr uint32_t X_NOGEN = 1u << 8;    // no generic parse (fast path or abort)
+constexpr uint32_t X_NOV6 = 1u << 9;     // no IPv6 / NDISC lookups
+constexpr uint32_t X_NOPORT = 1u << 10;  // no port lookups
+constexpr uint32_t X_NOCNT = 1u << 11;   // no counter bump code
 
 constexpr uint32_t M_SRC = 1, M_DST = 2, M_TCP = 4, M_UDP = 8;
 constexpr uint32_t A_ABORTED = 0, A_DROP = 1, A_PASS = 2, A_NONE = 7;
@@ -210,10 +217,10 @@ __device__ __forceinline__ Parsed parse(const P &p)
 	r.pdst = r.psrc = 0;
 	if (parse_fast<FEAT, W, P>(p, r))
 		return r;
-#ifdef XFG_EXP_NO_GENERIC
-	r.abort_at = ST_ETH;
-	return r;
-#endif
+	if constexpr ((FEAT & X_NOGEN) != 0) {
+		r.abort_at = ST_ETH;
+		return r;
+	}
 	const uint32_t len = p.len;
 
 	// parse_ethhdr (parsing_helpers.h:100-134), VLAN_MAX_DEPTH 4
@@ -552,12 +559,32 @@ __device__ __forceinline__ bool can_hit(uint32_t fmask, uint32_t m)
 	return (fmask & m) == m;
 }
 
-__device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s_pbits,
+// s_ports: the port table (kargs.port_tab) or, without one, the "any flag"
+// bitmap in front of a port_flags read.
+__device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s_ports,
 					   uint32_t key, uint32_t mask, uint32_t &tag)
 {
-	if (!can_hit(a.port_fmask, mask) || !((s_pbits[key >> 5] >> (key & 31)) & 1))
+	if (!can_hit(a.port_fmask, mask))
 		return false;
-	if ((a.port_flags[key] & mask) == mask) {
+	uint32_t f = 0;
+	if (a.port_tab) {
+		uint32_t sl = xfg_port_slot(key);
+		for (uint32_t d = 0; d <= a.port_tab_disp; d++) {
+			const uint32_t e = s_ports[sl];
+			if (e == 0)
+				break;
+			if ((e & 0xffff) == key) {
+				f = e >> 16;
+				break;
+			}
+			sl = (sl + 1) & (XFG_PORT_TAB - 1);
+		}
+	} else {
+		if (!((s_ports[key >> 5] >> (key & 31)) & 1))
+			return false;
+		f = a.port_flags[key];
+	}
+	if ((f & mask) == mask) {
 		tag = a.gbase[3] + key;
 		return true;
 	}
@@ -613,7 +640,7 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, co
 				return HIT;
 		}
 	}
-	if constexpr ((FEAT & F_IPV6) != 0) {
+	if constexpr ((FEAT & F_IPV6) != 0 && (FEAT & X_NOV6) == 0) {
 		if (a.t6.count && r.l3 == 3) {
 			// lookup_verdict_ipv6: dst then src (xdpfilt_prog.h:152-165)
 			Probe<6, NT> d, s;
@@ -629,7 +656,7 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, co
 	}
 	if (r.abort_at == ST_ND)
 		return A_ABORTED;
-	if constexpr ((FEAT & F_IPV6) != 0) {
+	if constexpr ((FEAT & F_IPV6) != 0 && (FEAT & X_NOV6) == 0) {
 		if (a.t6.count && r.nd) {
 			// NDISC target: NS => DST, NA => SRC (xdpfilt_prog.h:277-285)
 			const uint32_t mt = r.nd == 135 ? M_DST : M_SRC;
@@ -643,7 +670,7 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, co
 	}
 	if (r.abort_at == ST_L4)
 		return A_ABORTED;
-	if constexpr ((FEAT & (F_UDP | F_TCP)) != 0) {
+	if constexpr ((FEAT & (F_UDP | F_TCP)) != 0 && (FEAT & X_NOPORT) == 0) {
 		if (a.port_count && r.l4proto) {
 			// lookup_verdict_udp / _tcp (xdpfilt_prog.h:92-101 / :76-85)
 			const uint32_t pm = r.l4proto == 17 ? M_UDP : M_TCP;
@@ -678,6 +705,34 @@ __device__ __forceinline__ bool cache_hit(uint32_t *s_ctag, uint32_t *s_ccnt, ui
 	return true;
 }
 
+
+// Diagnostics (build variant V & 4): per-workgroup cycles spent in each
+// phase of the tile loop, stamped by wave 0 and written to kargs.prof.
+constexpr int NPHASE = 8;
+struct Stamps {
+	unsigned long long last;
+	uint32_t *acc;   // LDS, NPHASE words
+	__device__ __forceinline__ void init(uint32_t *lds)
+	{
+		acc = lds;
+		if (threadIdx.x < NPHASE)
+			acc[threadIdx.x] = 0;
+		last = __builtin_amdgcn_s_memtime();
+	}
+	__device__ __forceinline__ void mark(int i)
+	{
+		const unsigned long long t = __builtin_amdgcn_s_memtime();
+		if (threadIdx.x == 0)
+			acc[i] += (uint32_t)(t - last);
+		last = t;
+	}
+	__device__ __forceinline__ void store(unsigned long long *prof) const
+	{
+		if (prof && threadIdx.x == 0 && blockIdx.x < XFG_PROF_WG)
+			for (int i = 0; i < NPHASE; i++)
+				prof[(uint64_t)blockIdx.x * NPHASE + i] = acc[i];
+	}
+};
 
 __device__ __forceinline__ uint32_t load_len(const xfg_kargs &a, uint64_t i)
 {
@@ -715,7 +770,7 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 	if constexpr (PORTS) {
 		if (a.port_count)
 			for (int i = tid; i < 2048; i += TILE)
-				s_pbits[i] = a.port_bits[i];
+				s_pbits[i] = a.port_tab ? a.port_tab[i] : a.port_bits[i];
 	}
 	// fixed-stride layout with stride >= W: every window byte is readable,
 	// so loads need no length (no load->load dependency on the stream)
@@ -755,12 +810,19 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 	if (tile < ntiles)
 		issue(tile);
 #endif
+	constexpr bool PROF = (V & 4) != 0;
+	__shared__ uint32_t s_prof[PROF ? NPHASE : 1];
+	Stamps st;
+	if constexpr (PROF)
+		st.init(s_prof);
 
 	for (; tile < ntiles; tile += gridDim.x) {
 		const uint64_t base = tile * TILE;
 #ifdef XFG_EXP_NO_PREFETCH
 		issue(tile);
 #endif
+		if constexpr (PROF)
+			st.mark(7);   // end-of-tile bookkeeping + loop
 		// 1. stage the prefetched windows into LDS
 #pragma unroll
 		for (int it = 0; it < CPP; it++) {
@@ -773,11 +835,19 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 			dst[3] = pre[it].w;
 		}
 		const uint32_t len = plen;
+		if constexpr (PROF) {
+			asm volatile("" ::"v"(len));
+			st.mark(0);   // prefetched windows landed and written to LDS
+		}
 		__syncthreads();
+		if constexpr (PROF)
+			st.mark(1);   // barrier
 #ifndef XFG_EXP_NO_PREFETCH
 		if (tile + gridDim.x < ntiles)
 			issue(tile + gridDim.x);   // next tile's stream overlaps this tile's work
 #endif
+		if constexpr (PROF)
+			st.mark(2);   // next tile issued
 
 		// 2-4. parse, match, verdict
 		const uint64_t gi = base + tid;
@@ -789,11 +859,21 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 				act = p.u8(0) & 1;
 			} else {
 				const Parsed r = parse<FEAT, W>(p);
+				if constexpr (PROF) {
+					asm volatile("" ::"v"(r.abort_at), "v"(r.k4a), "v"(r.l3));
+					st.mark(3);   // parse
+				}
 				act = lookups<FEAT, (V & 1) != 0>(a, LazyKeys<Pkt<W>>{ p }, r, s_pbits, tag);
+			}
+			if constexpr (PROF) {
+				asm volatile("" ::"v"(act), "v"(tag));
+				st.mark(4);   // lookups
 			}
 			a.verdicts[gi] = (uint8_t)act;
 		}
 		if (a.ablate & 2)
+			tag = CT_NONE;
+		if constexpr ((FEAT & X_NOCNT) != 0)
 			tag = CT_NONE;
 
 		// counter bump: lanes of the wave hitting the same rule are merged
@@ -833,8 +913,14 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 			c_pa++;
 			b_pa += len;
 		}
+		if constexpr (PROF)
+			st.mark(5);   // counters, verdict, stats
 		__syncthreads();   // LDS window reuse
+		if constexpr (PROF)
+			st.mark(6);   // end barrier
 	}
+	if constexpr (PROF)
+		st.store(a.prof);
 	// per-action stats: lane sums -> wave sums -> workgroup (LDS) -> device
 	{
 		unsigned long long v[6] = { c_ab, b_ab, c_dr, b_dr, c_pa, b_pa };
@@ -901,6 +987,20 @@ template <int N>
 __device__ __forceinline__ void wait_vm()
 {
 	asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Wait until at most y (wave-uniform, <= 23) vector-memory operations of this
+// wave are outstanding.
+__device__ __forceinline__ void wait_vm_dyn(uint32_t y)
+{
+	switch (y) {
+#define XFG_W(n) case n: wait_vm<n>(); break;
+	XFG_W(1) XFG_W(2) XFG_W(3) XFG_W(4) XFG_W(5) XFG_W(6) XFG_W(7) XFG_W(8)
+	XFG_W(9) XFG_W(10) XFG_W(11) XFG_W(12) XFG_W(13) XFG_W(14) XFG_W(15) XFG_W(16)
+	XFG_W(17) XFG_W(18) XFG_W(19) XFG_W(20) XFG_W(21) XFG_W(22) XFG_W(23)
+#undef XFG_W
+	default: wait_vm<0>(); break;
+	}
 }
 
 // Workgroup barrier that waits for this wave's LDS operations only (an LDS-
@@ -1013,7 +1113,7 @@ __global__ __launch_bounds__(IO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 	if constexpr (PORTS) {
 		if (a.port_count)
 			for (int i = tid; i < 2048; i += IO_THREADS)
-				s_pbits[i] = a.port_bits[i];
+				s_pbits[i] = a.port_tab ? a.port_tab[i] : a.port_bits[i];
 	}
 
 	const uint64_t ntiles = (a.n + TILE - 1) / TILE;
@@ -1024,35 +1124,56 @@ __global__ __launch_bounds__(IO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 	const uint32_t lens_lds = __builtin_amdgcn_readfirstlane(lds_addr(&s_lens[0][0]));
 	const uint32_t esz = a.lens_u16 ? 2 : 4;
 
-	// I/O wave: 17 LDS-DMA instructions per tile (16 window KiBs + lengths)
+	// I/O wave: 17 LDS-DMA instructions per tile (16 window KiBs + lengths).
+	// Instruction j, lane l loads packet 16j + l/4, chunk c(l) = (l & 3) ^
+	// ((l >> 4) & 3) (the swizzle; independent of j), so a lane's source
+	// address advances by 16 packets per instruction.
+	const uint64_t io_off = (uint64_t)(lane >> 2) * a.stride + 16u * ((lane & 3) ^ ((lane >> 4) & 3));
 	auto io_issue = [&](uint64_t k) {
 		const uint64_t p0 = (b + k * G) * TILE;
-		const uint32_t buf = (uint32_t)(k & 1);
+		const uint32_t ldsb = ring_lds + (uint32_t)(k & 1) * (SBUF_DW * 4);
+		const uint64_t step = 16ull * a.stride;
+		const uint8_t *src = a.data + p0 * a.stride + io_off;
+		if (p0 + TILE <= a.n) {
 #pragma unroll
-		for (int j = 0; j < 16; j++) {
-			const uint32_t s = j * 64 + lane;
-			const uint32_t p = s >> 2;
-			const uint32_t c = (s & 3) ^ ((p >> 2) & 3);
-			const uint64_t gi = p0 + p;
-			const uint8_t *src = gi < a.n ? a.data + gi * a.stride + c * 16 : a.data;
-			glds16(src, ring_lds + buf * (SBUF_DW * 4) + j * 1024);
+			for (int j = 0; j < 16; j++) {
+				glds16(src, __builtin_amdgcn_readfirstlane(ldsb + j * 1024));
+				src += step;
+			}
+		} else {
+#pragma unroll
+			for (int j = 0; j < 16; j++) {
+				const uint64_t gi = p0 + 16 * j + (lane >> 2);
+				glds16(gi < a.n ? src : a.data, __builtin_amdgcn_readfirstlane(ldsb + j * 1024));
+				src += step;
+			}
 		}
 		const uint64_t first = p0 + (uint64_t)lane * (16 / esz);
 		const uint8_t *lsrc = static_cast<const uint8_t *>(a.lens);
 		if (lane < (a.lens_u16 ? 32 : 64))
-			glds16(first < a.n ? lsrc + first * esz : lsrc, lens_lds + buf * (TILE * 4));
+			glds16(first < a.n ? lsrc + first * esz : lsrc,
+			       __builtin_amdgcn_readfirstlane(lens_lds + (uint32_t)(k & 1) * (TILE * 4)));
 	};
-	// I/O wave: counter atomics and verdict bytes of tile k (LDS parity k & 1)
-	auto io_flush = [&](uint64_t k) {
+	// I/O wave: counter atomics and verdict bytes of tile k (LDS parity
+	// k & 1).  Returns a lower bound of the vector-memory instructions it
+	// issued (exact on full tiles): one per 64 queued bumps, one store.
+	auto io_flush = [&](uint64_t k) -> uint32_t {
 		const uint32_t q = (uint32_t)(k & 1);
-		const uint32_t nq = s_qn[q];
-		if (!(a.ablate & 2))
-			for (uint32_t i = lane; i < nq; i += 64)
-				atomicAdd(global_counter(a, s_q[q][i]), 1ull);
+		const uint32_t nq = (a.ablate & 2) ? 0 : s_qn[q];
+		uint32_t ops = 0;
+#pragma unroll
+		for (uint32_t i = 0; i < TILE / 64; i++) {
+			if (i * 64 < nq) {   // wave-uniform: lane 0 is active below
+				ops++;
+				if (i * 64 + lane < nq)
+					atomicAdd(global_counter(a, s_q[q][i * 64 + lane]), 1ull);
+			}
+		}
 		const uint64_t p0 = (b + k * G) * TILE;
 		const uint32_t v = s_verd[q][lane];
 		if (p0 + TILE <= a.n && !((uintptr_t)a.verdicts & 3)) {
 			reinterpret_cast<uint32_t *>(a.verdicts + p0)[lane] = v;
+			ops++;
 		} else {
 #pragma unroll
 			for (int i = 0; i < 4; i++)
@@ -1061,6 +1182,7 @@ __global__ __launch_bounds__(IO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 		}
 		if (lane == 0)
 			s_qn[q] = 0;
+		return ops;
 	};
 
 	uint32_t c_ab = 0, c_dr = 0, c_pa = 0;
@@ -1082,16 +1204,15 @@ __global__ __launch_bounds__(IO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 		const uint32_t par = (uint32_t)(k & 1);
 		if (io) {
 			wg_barrier();   // P_k: tile k parsed, its buffer free
+			// issue order F(k-1), I(k+2): wait for I(k+1) (issued a step
+			// ago, older than both) and whatever preceded it
+			uint32_t younger = k >= 1 ? io_flush(k - 1) : 0;
 			if (k + 2 < K) {
 				io_issue(k + 2);
-				if (k >= 1)
-					io_flush(k - 1);
-				wait_vm<17>();   // tile k+1 (and the flush before it) landed
-			} else {
-				if (k >= 1)
-					io_flush(k - 1);
-				wait_vm<0>();
+				younger += 17;
 			}
+			if (k + 1 < K)
+				wait_vm_dyn(younger);
 			wg_barrier();   // E_k
 			continue;
 		}
@@ -1231,6 +1352,16 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 			case 3:
 				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 3>), dim3(grid), dim3(TILE), 0, s, a);
 				return hipGetLastError();
+			case 4:
+				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 4>), dim3(grid), dim3(TILE), 0, s, a);
+				return hipGetLastError();
+#define XFG_XV(x)                                                                              \
+			case x:                                                                \
+				hipLaunchKernelGGL((xfg_classify_kernel<FEAT | x, 64, 0>), dim3(grid), \
+						   dim3(TILE), 0, s, a);                       \
+				return hipGetLastError();
+			XFG_XV(0x100) XFG_XV(0x200) XFG_XV(0x400) XFG_XV(0x800) XFG_XV(0xF00)
+#undef XFG_XV
 			default:
 				break;
 			}

@@ -58,6 +58,11 @@
 
 #define XFG_META_OVERFLOW 1u
 
+#define XFG_PROF_WG 8192u  /* diagnostics: workgroups with a phase-cycle record */
+
+#define XFG_PORT_TAB      2048u   /* LDS port table slots (8 KiB, the bitmap's size) */
+#define XFG_PORT_TAB_MAX  1024u   /* at most this many ruled ports use the table */
+
 #define XFG_BLOOM_K       4u
 
 /* Per-hash-map descriptor passed to the kernel by value. */
@@ -97,6 +102,12 @@ struct xfg_kargs {
 	uint32_t variant;             /* diagnostics only (XFG_VARIANT env): build variant */
 	uint32_t port_fmask;          /* OR of the port flag bytes (see tdesc.fmask) */
 	uint32_t streamed;            /* 1: the streamed kernel (I/O wave + lookup waves) */
+	unsigned long long *prof;     /* diagnostics: per-workgroup phase cycles (variant 4) */
+	/* Ruled ports as a small open-addressed table each workgroup copies to
+	 * LDS (NULL when more than XFG_PORT_TAB_MAX ports carry flags: then the
+	 * bitmap above plus a port_flags read) */
+	const uint32_t *port_tab;     /* XFG_PORT_TAB entries: flags << 16 | key, 0 = empty */
+	uint32_t port_tab_disp;       /* longest probe displacement in the table */
 	/* Global counter index space (the LDS counter cache's tags): v4 slots,
 	 * v6 slots, eth slots (each with its zero-key slot), then the 65536
 	 * ports; gbase[i] = first index of each. */
@@ -157,6 +168,12 @@ XFG_HD unsigned long long xfg_bloom_mask(uint32_t h)
 	uint32_t g = xfg_fmix32(h ^ 0x7f4a7c15u);
 	return (1ull << (g & 63)) | (1ull << ((g >> 6) & 63)) | (1ull << ((g >> 12) & 63)) |
 	       (1ull << ((g >> 18) & 63));
+}
+
+/* Home slot of a port key in the LDS port table. */
+XFG_HD uint32_t xfg_port_slot(uint32_t key)
+{
+	return (key * 0x9E3779B1u) >> 21;   /* 11 bits: XFG_PORT_TAB slots */
 }
 
 #endif /* XFG_LAYOUT_H */
