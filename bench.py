@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline duration (0 disables)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--host-log2-packets", type=int, default=22,
+                    help="sample for the PCIe-inclusive host-buffer rate (0 disables)")
     return ap.parse_args()
 
 
@@ -103,6 +105,26 @@ def main():
     peak_meas_ms = f.stream_read_timed(d_data.ptr, n * stride, 5)
     peak_meas = n * stride / (peak_meas_ms * 1e-3) / 1e9
 
+    # ---- PCIe-inclusive rate: the same workload handed over in host memory
+    # (xfg_classify_host: pinned staging, H2D, classify, D2H of verdicts);
+    # reported beside `value`, never as it
+    host_path = None
+    if rank == 0 and args.host_log2_packets > 0:
+        hn = 1 << args.host_log2_packets
+        hdata, hlens = X.gen_workload(7, 3, hn, stride, v4=v4, ports=ports, dst_permille=500,
+                                      port_permille=250, bad_permille=10)
+        f.classify_host(hdata, hlens, stride=stride)          # warm the staging buffers
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            f.classify_host(hdata, hlens, stride=stride)
+        hs = (time.perf_counter() - t0) / reps
+        host_path = {"Mpps": round(hn / hs / 1e6, 1), "packets": hn, "ms": round(hs * 1e3, 3),
+                     "GBps_h2d": round(hdata.nbytes / hs / 1e9, 1),
+                     "note": "host-resident batch incl. H2D frames+lens and D2H verdicts "
+                             "(xfg_classify_host, double-buffered pinned staging)"}
+        del hdata
+
     # ---- CPU baseline (rank 0, N=1 only)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0:
@@ -150,6 +172,8 @@ def main():
     }
     if reduce_ms is not None:
         line["reduce_ms"] = round(reduce_ms, 3)
+    if host_path is not None:
+        line["host_path"] = host_path
     if rank == 0:
         print(json.dumps(line), flush=True)
     f.close()

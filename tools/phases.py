@@ -42,7 +42,7 @@ def main():
         if a.grid_per_cu:
             os.environ["XFG_GRID_PER_CU"] = a.grid_per_cu
         plain = f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, 5, lens_u16=True)
-        os.environ["XFG_VARIANT"] = "4"
+        os.environ["XFG_VARIANT"] = os.environ.get("PHASES_VARIANT", "4")
         buf = (C.c_uint64 * (8192 * 8))()
         G.lib.xfg_diag_prof(f.ctx, 0, buf, 8192 * 8)      # clear
         prof_ms = f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, 1, lens_u16=True)

@@ -776,26 +776,34 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 	// so loads need no length (no load->load dependency on the stream)
 	const bool guarded = a.offsets != nullptr || a.stride < (uint32_t)W;
 
-	const uint64_t ntiles = (a.n + TILE - 1) / TILE;
+	// WT (V & 8): every wave walks its own tiles of 64 packets with its own
+	// LDS rows, so no workgroup barrier sits in the loop; otherwise tiles of
+	// TILE packets shared by the workgroup's four waves.
+	constexpr bool WT = (V & 8) != 0;
+	constexpr int U = WT ? 64 : TILE;          // packets per tile
+	const int me = WT ? lane : tid;            // this lane's packet within the tile
+	uint32_t *const wrows = WT ? win + (tid >> 6) * 64 * ROWDW : win;
+	const uint64_t ntiles = (a.n + U - 1) / U;
+	const uint64_t tstep = WT ? (uint64_t)gridDim.x * (TILE / 64) : gridDim.x;
 	// dense layout (stride == W, no offsets): a tile is one contiguous block
-	// of TILE * W bytes and chunk c of it sits at byte 16 * c
+	// of U * W bytes and chunk c of it sits at byte 16 * c
 	const bool dense = !guarded && a.stride == (uint32_t)W;
-	uint64_t tile = blockIdx.x;
+	uint64_t tile = WT ? (uint64_t)blockIdx.x * (TILE / 64) + (tid >> 6) : blockIdx.x;
 	u32x4 pre[CPP];
 	uint32_t plen = 0;
 	uint32_t c_ab = 0, c_dr = 0, c_pa = 0;
 	unsigned long long b_ab = 0, b_dr = 0, b_pa = 0;
 	auto issue = [&](uint64_t t) {
-		const uint64_t base = t * TILE;
-		if (dense && base + TILE <= a.n) {
-			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + base * W) + tid;
+		const uint64_t base = t * U;
+		if (dense && base + U <= a.n) {
+			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + base * W) + me;
 #pragma unroll
 			for (int it = 0; it < CPP; it++)
-				pre[it] = __builtin_nontemporal_load(src + it * TILE);
+				pre[it] = __builtin_nontemporal_load(src + it * U);
 		} else {
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
-				const int c = it * TILE + tid;
+				const int c = it * U + me;
 				const int pk = c / CPP, sub = c % CPP;
 				const uint64_t gi = base + pk;
 				pre[it] = u32x4{ 0, 0, 0, 0 };
@@ -804,7 +812,13 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 						reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16));
 			}
 		}
-		plen = base + tid < a.n ? load_len(a, base + tid) : 0;
+		plen = base + me < a.n ? load_len(a, base + me) : 0;
+	};
+	auto tile_sync = [&]() {
+		if constexpr (WT)
+			__builtin_amdgcn_wave_barrier();   // rows are this wave's own
+		else
+			__syncthreads();
 	};
 #ifndef XFG_EXP_NO_PREFETCH
 	if (tile < ntiles)
@@ -816,8 +830,8 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 	if constexpr (PROF)
 		st.init(s_prof);
 
-	for (; tile < ntiles; tile += gridDim.x) {
-		const uint64_t base = tile * TILE;
+	for (; tile < ntiles; tile += tstep) {
+		const uint64_t base = tile * U;
 #ifdef XFG_EXP_NO_PREFETCH
 		issue(tile);
 #endif
@@ -826,9 +840,9 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 		// 1. stage the prefetched windows into LDS
 #pragma unroll
 		for (int it = 0; it < CPP; it++) {
-			const int c = it * TILE + tid;
+			const int c = it * U + me;
 			const int pk = c / CPP, sub = c % CPP;
-			uint32_t *dst = &win[pk * ROWDW + sub * 4];
+			uint32_t *dst = &wrows[pk * ROWDW + sub * 4];
 			dst[0] = pre[it].x;
 			dst[1] = pre[it].y;
 			dst[2] = pre[it].z;
@@ -839,22 +853,22 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 			asm volatile("" ::"v"(len));
 			st.mark(0);   // prefetched windows landed and written to LDS
 		}
-		__syncthreads();
+		tile_sync();
 		if constexpr (PROF)
 			st.mark(1);   // barrier
 #ifndef XFG_EXP_NO_PREFETCH
-		if (tile + gridDim.x < ntiles)
-			issue(tile + gridDim.x);   // next tile's stream overlaps this tile's work
+		if (tile + tstep < ntiles)
+			issue(tile + tstep);   // next tile's stream overlaps this tile's work
 #endif
 		if constexpr (PROF)
 			st.mark(2);   // next tile issued
 
 		// 2-4. parse, match, verdict
-		const uint64_t gi = base + tid;
+		const uint64_t gi = base + me;
 		uint32_t act = A_NONE;
 		uint32_t tag = CT_NONE;
 		if (gi < a.n) {
-			Pkt<W> p{ &win[tid * ROWDW], pkt_ptr(a, gi), len };
+			Pkt<W> p{ &wrows[me * ROWDW], pkt_ptr(a, gi), len };
 			if (a.ablate & 4) {
 				act = p.u8(0) & 1;
 			} else {
@@ -915,7 +929,7 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 		}
 		if constexpr (PROF)
 			st.mark(5);   // counters, verdict, stats
-		__syncthreads();   // LDS window reuse
+		tile_sync();   // LDS window reuse
 		if constexpr (PROF)
 			st.mark(6);   // end barrier
 	}
@@ -1354,6 +1368,12 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 				return hipGetLastError();
 			case 4:
 				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 4>), dim3(grid), dim3(TILE), 0, s, a);
+				return hipGetLastError();
+			case 8:
+				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 8>), dim3(grid), dim3(TILE), 0, s, a);
+				return hipGetLastError();
+			case 12:
+				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 12>), dim3(grid), dim3(TILE), 0, s, a);
 				return hipGetLastError();
 #define XFG_XV(x)                                                                              \
 			case x:                                                                \
