@@ -116,6 +116,12 @@ int xfg_map_lookup(xfg_ctx *ctx, int map, const void *key, uint64_t *vals);
 int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals);
 int xfg_map_delete(xfg_ctx *ctx, int map, const void *key);
 int xfg_map_get_next_key(xfg_ctx *ctx, int map, const void *key, void *next_key);
+/* Bulk insert/overwrite with per-device values, as bpf_map_update_elem()
+ * takes one value per possible CPU: vals[i * nvals + d] is device d's value
+ * of key i (nvals = max(xfg_num_devices(), 1)).  The rule store reloads
+ * saved hit counts onto one device with it (xdpfilter_io.h). */
+int xfg_map_update_batch_percpu(xfg_ctx *ctx, int map, const void *keys,
+				const uint64_t *vals, uint64_t n);
 /* Number of keys present (ports: number of non-zero entries). */
 int64_t xfg_map_count(xfg_ctx *ctx, int map);
 /* Bulk lookup of @n keys (status readout, parity checks): vals[i*ndev + d]

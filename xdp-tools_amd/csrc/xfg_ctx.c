@@ -767,20 +767,23 @@ out:
 	return err ? err : found;
 }
 
-int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t *vals,
-			 uint64_t n)
+/* vals[i] on every device (percpu = 0) or vals[i * nvals + d] (percpu = 1). */
+static int update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t *vals,
+			uint64_t n, int percpu)
 {
 	int err = 0, kl = keylen_of(map);
 	if (!ctx || (!keys && n) || (!vals && n) || kl < 0)
 		return -EINVAL;
+	const int nv = ctx->ndev ? ctx->ndev : 1;
+#define VAL(i, d) (percpu ? vals[(i) * (uint64_t)nv + (d)] : vals[i])
 	if (map == XFG_MAP_PORTS) {
 		uint64_t v[64];
 		uint64_t *vv = ctx->ndev > 64 ? calloc(ctx->ndev, 8) : v;
 		if (!vv)
 			return -ENOMEM;
 		for (uint64_t i = 0; i < n && !err; i++) {
-			for (int d = 0; d < (ctx->ndev ? ctx->ndev : 1); d++)
-				vv[d] = vals[i];
+			for (int d = 0; d < nv; d++)
+				vv[d] = VAL(i, d);
 			err = xfg_map_update(ctx, map, (const uint8_t *)keys + 4 * i, vv);
 		}
 		if (vv != v)
@@ -827,16 +830,20 @@ int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t
 			err = (int)s;
 			break;
 		}
-		flags_note(ctx, mi, (uint64_t)s, vals[i] & 63);
+		uint8_t any = 0;
+		for (int d = 0; d < nv; d++)
+			any |= VAL(i, d) & 63;
+		flags_note(ctx, mi, (uint64_t)s, any);
 		if (nd) {
 			for (int d = 0; d < nd; d++) {
-				img[ib * d + xfg_table_flag_off(t, s)] = vals[i] & 63;
-				hits[ns * d + s] = vals[i] >> XFG_COUNTER_SHIFT;
+				img[ib * d + xfg_table_flag_off(t, s)] = VAL(i, d) & 63;
+				hits[ns * d + s] = VAL(i, d) >> XFG_COUNTER_SHIFT;
 			}
 		} else {
-			ctx->host_vals[mi][s] = vals[i];
+			ctx->host_vals[mi][s] = VAL(i, 0);
 		}
 	}
+#undef VAL
 	/* merge host keys + meta into each device image (flags stay per device)
 	 * and upload; also on partial failure: keys inserted so far stay */
 	for (int i = 0; i < nd; i++) {
@@ -860,6 +867,18 @@ out:
 	free(hits);
 	pthread_mutex_unlock(&ctx->lock);
 	return err;
+}
+
+int xfg_map_update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t *vals,
+			 uint64_t n)
+{
+	return update_batch(ctx, map, keys, vals, n, 0);
+}
+
+int xfg_map_update_batch_percpu(xfg_ctx *ctx, int map, const void *keys, const uint64_t *vals,
+				uint64_t n)
+{
+	return update_batch(ctx, map, keys, vals, n, 1);
 }
 
 /* ------------------------------------------------------------------ classify */
