@@ -163,6 +163,29 @@ int xfg_classify(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
 		 uint8_t *verdicts, void *stream);
 
 /*
+ * AF_XDP descriptors in device memory: packet i is RX ring
+ * record descs[(first + i) & mask], a struct xdp_desc {u64 addr; u32 len;
+ * u32 options} (headers/linux/if_xdp.h:110-114, read with
+ * xsk_ring_cons__rx_desc(), headers/xdp/xsk.h:79-85), over the UMEM at
+ * @umem: its bytes start at umem + (addr & ((1 << 48) - 1)) + (addr >> 48)
+ * (xsk_umem__add_offset_to_addr(), headers/xdp/xsk.h:173-186) and it is len
+ * bytes long.  mask = ring entries - 1 (a power of two), or 0xffffffff for
+ * a plain array.  Frame starts must be 16-byte aligned (default UMEM frame
+ * sizes and headroom are) and readable up to the next 16-byte boundary past
+ * their end.  Single-buffer descriptors only (XDP_PKT_CONTD clear).
+ */
+struct xfg_desc_batch {
+	const void *umem;
+	const void *descs;
+	uint32_t first;
+	uint32_t mask;
+	uint64_t count;
+};
+
+int xfg_classify_descs(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *batch,
+		       uint8_t *verdicts, void *stream);
+
+/*
  * Host-resident batch: copies packets to the device (pinned staging,
  * pipelined H2D / kernel / D2H over chunks), classifies, copies verdicts
  * back.  Packet layout as struct xfg_batch but in host memory.

@@ -20,13 +20,16 @@ import xftools as X
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_library_exports_every_declared_symbol():
-    hdr = open(os.path.join(ROOT, "include", "xdpfilter_gpu.h")).read()
+@pytest.mark.parametrize("header,listed", [("xdpfilter_gpu.h", "EXPORTS"),
+                                           ("xdpfilter_io.h", "IO_EXPORTS")])
+def test_library_exports_every_declared_symbol(header, listed):
+    hdr = open(os.path.join(ROOT, "include", header)).read()
     declared = set(re.findall(r"\b(xfg_[a-z0-9_]+)\s*\(", hdr))
     assert declared, "no declarations parsed"
     missing = [s for s in sorted(declared) if not hasattr(G.lib, s)]
     assert not missing, f"not exported: {missing}"
-    assert declared <= set(G.EXPORTS) | {"xfg_stream_read_timed"}
+    assert set(getattr(G, listed)) <= declared
+    assert declared <= set(G.EXPORTS) | set(G.IO_EXPORTS)
 
 
 def test_native_library_is_the_in_tree_build():

@@ -1,0 +1,230 @@
+"""CPU tests of the xdp-filter command line (xdp-tools_amd/bin/xdp-filter)
+against a temporary state directory.  Each test restates a reference test:
+
+  test_load / test_print / test_output_remove   xdp-filter/tests/test-xdp-filter.sh:28-54,
+                                                295-351
+  Status.*                                      xdp-filter/tests/test_basic.py:235-279
+  map capacity overflow                         xdp-filter/tests/test_slow.py (first address
+                                                that fails to insert must not be stored)
+plus the map value algebra of map_get_counter_flags()/map_set_flags()
+(xdp-filter/xdp-filter.c:73-157) and the load/unload pinning rules (:253-548).
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import xfgpu as G
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+XF = os.path.join(ROOT, "xdp-tools_amd", "bin", "xdp-filter")
+
+
+@pytest.fixture
+def cli(tmp_path):
+    state = str(tmp_path / "state")
+    env = dict(os.environ, XDP_FILTER_STATE_DIR=state)
+
+    def run(*args, ok=True):
+        p = subprocess.run([XF, *map(str, args)], env=env, capture_output=True, text=True,
+                           timeout=60)
+        if ok is True:
+            assert p.returncode == 0, (args, p.stdout, p.stderr)
+        elif ok is False:
+            assert p.returncode != 0, (args, p.stdout, p.stderr)
+        return p
+    run.state = state
+    return run
+
+
+def status(cli):
+    return cli("status").stdout
+
+
+def test_load_selects_program_like_find_prog_file(cli):
+    # test-xdp-filter.sh:28-54 (program names without the .o suffix)
+    feats = ["tcp", "udp", "ipv4", "ipv6", "ethernet", "all"]
+    allow = ["alw_tcp", "alw_udp", "alw_ip", "alw_ip", "alw_eth", "alw_all"]
+    for f, a in zip(feats, allow):
+        for extra, prog in (([], a), (["--mode", "skb"], a), (["--policy", "deny"], a.replace("alw", "dny")),
+                            (["--policy", "deny", "--mode", "skb"], a.replace("alw", "dny"))):
+            p = cli("load", "veth0", "--features", f, *extra, "-v")
+            assert f"Found prog 'xdpfilt_{prog}'" in p.stderr
+            cli("unload", "veth0", "-v")
+    assert not os.path.exists(cli.state)        # last unload removes the pin directory
+    p = cli("load", "veth0", "-f", "tcp,udp", "-v")
+    assert "Found prog 'xdpfilt_alw_all'" in p.stderr   # first superset in Makefile order
+    cli("unload", "veth0")
+
+
+def test_print(cli):
+    # test-xdp-filter.sh:295-307
+    cli("load", "veth0", "-v")
+    cli("ether", "aa:bb:cc:dd:ee:ff")
+    assert "aa:bb:cc:dd:ee:ff" in status(cli)
+    cli("ip", "1.2.3.4")
+    assert "1.2.3.4" in status(cli)
+    cli("ip", "aa::bb")
+    assert "aa::bb" in status(cli)
+    cli("port", "100")
+    assert re.search(r"100.*dst,tcp,udp", status(cli))
+    cli("unload", "veth0", "-v")
+
+
+@pytest.mark.parametrize("opts,expect", [
+    ("-m src", "dst,tcp,udp"), ("-m dst", "src,tcp,udp"), ("-p udp", "src,dst,tcp"),
+    ("-p tcp", "src,dst,udp"), ("-m src -p udp", "dst,tcp"), ("-m src -p tcp", "dst,udp"),
+    ("-m dst -p udp", "src,tcp"), ("-m dst -p tcp", "src,udp"), ("", ""), ("-m src,dst", ""),
+    ("-p tcp,udp", ""), ("-m src,dst -p tcp,udp", "")])
+def test_output_remove(cli, opts, expect):
+    # test-xdp-filter.sh:309-351
+    cli("load", "veth0")
+    cli("port", 54321, "-p", "tcp,udp", "-m", "src,dst")
+    assert re.search(r"54321.*src,dst,tcp,udp", status(cli))
+    cli("port", 54321, *opts.split(), "-r")
+    if expect:
+        assert re.search(r"54321\s+" + expect + r"\s", status(cli))
+    else:
+        assert "54321" not in status(cli)
+    cli("unload", "veth0")
+
+
+@pytest.mark.parametrize("features,cmds", [
+    ("ethernet", [("ether", "02:00:00:00:00:01")]), ("ipv4", [("ip", "10.11.1.1")]),
+    ("udp", [("port", "10000")]),
+    ("all", [("ether", "02:00:00:00:00:01"), ("ip", "10.11.1.1"), ("port", "10000")])])
+def test_status_add_remove(cli, features, cmds):
+    # test_basic.py:235-279
+    cli("load", "veth0", "--features", features)
+    for sub, addr in cmds:
+        assert addr not in status(cli)
+        cli(sub, addr)
+        assert addr in status(cli)
+        cli(sub, addr, "--remove")
+        assert addr not in status(cli)
+    cli("unload", "veth0")
+
+
+def test_status_layout(cli):
+    cli("load", "eth7", "-p", "deny", "-m", "skb")
+    cli("port", 53, "-m", "src")
+    cli("ip", "10.0.0.1", "-m", "src,dst")
+    out = status(cli).splitlines()
+    assert out[:2] == ["CURRENT XDP-FILTER STATUS:", ""]
+    assert out[2] == "Aggregate per-action statistics:"
+    assert re.fullmatch(r"  XDP_ABORTED\s+0 pkts\s+0 KiB", out[3])
+    assert out[6:10] == ["", "Loaded on interfaces:", "  " + " " * 40 + " Enabled features",
+                         "xdpfilt_dny_all"]
+    assert out[10] == "  " + "eth7 (skb mode)".ljust(40) + " tcp,udp,ipv6,ipv4,ethernet,deny"
+    assert "Filtered ports:" in out and "Filtered IP addresses:" in out
+    assert "  " + "53".ljust(40) + " " + "src,tcp,udp".ljust(15) + "  0" in out
+    assert "  " + "10.0.0.1".ljust(40) + " " + "src,dst".ljust(15) + "  0" in out
+    cli("unload", "eth7")
+
+
+def test_features_pin_only_their_maps(cli):
+    cli("load", "veth0", "-f", "ipv4")
+    assert "Filtered ports:" not in status(cli)
+    p = cli("port", 80, ok=False)
+    assert "Couldn't find port filter map" in p.stderr
+    p = cli("ether", "aa:bb:cc:dd:ee:ff", ok=False)
+    assert "ethernet feature" in p.stderr
+    cli("ip", "::1")       # -f ipv4 selects xdpfilt_alw_ip, which pins filter_ipv6 too
+    cli("ip", "192.168.0.1")
+    cli("unload", "veth0")
+    assert not os.path.exists(cli.state)
+
+
+def test_policy_conflicts_and_double_load(cli):
+    cli("load", "a0", "-p", "deny")
+    p = cli("load", "a1", ok=False)
+    assert "already loaded in deny policy mode" in p.stderr
+    p = cli("load", "a0", "-p", "deny", ok=False)
+    assert "already loaded on a0" in p.stderr
+    cli("load", "a1", "-p", "deny", "-f", "tcp")
+    p = cli("load", "a2", "-m", "hw", ok=False)
+    assert "does not support offloading" in p.stderr
+    out = status(cli)
+    assert "xdpfilt_dny_all" in out and "xdpfilt_dny_tcp" in out
+    cli("unload", "a0")
+    cli("unload", "a1")
+    assert not os.path.exists(cli.state)
+    p = cli("unload", "a1", ok=False)
+    assert "not loaded on a1" in p.stderr
+
+
+def test_unload_keeps_maps_in_use(cli):
+    cli("load", "a0", "-f", "ipv4")
+    cli("load", "a1", "-f", "tcp")
+    cli("ip", "1.1.1.1")
+    cli("port", 22)
+    cli("unload", "a1")                        # ports no longer used: removed
+    assert not G.lib.xfg_store_has_map(cli.state.encode(), G.MAP_PORTS)
+    assert "1.1.1.1" in status(cli)
+    cli("load", "a1", "-f", "tcp")
+    assert "22 " not in status(cli)             # a fresh port map
+    cli("port", 22)
+    cli("unload", "a1", "--keep-maps")
+    assert re.search(r"\b22\s+dst,tcp,udp", status(cli))
+    cli("unload", "--all")
+    assert not os.path.exists(cli.state)
+
+
+def test_ip_and_ether_value_algebra(cli):
+    cli("load", "veth0")
+    cli("ip", "10.0.0.1", "-m", "src")
+    cli("ip", "10.0.0.1")                       # default dst: flags OR
+    assert re.search(r"10\.0\.0\.1\s+src,dst\s", status(cli))
+    cli("ip", "10.0.0.1", "-r")                 # default dst removed
+    assert re.search(r"10\.0\.0\.1\s+src\s", status(cli))
+    cli("ip", "10.0.0.1", "-r", "-m", "src")    # no flags left: key deleted
+    assert "10.0.0.1" not in status(cli)
+    cli("ip", "::ffff:1.2.3.4")                 # IPv4-mapped IPv6 stays an IPv6 key
+    assert "::ffff:1.2.3.4" in status(cli)
+    cli("ether", "0A:0b:0C:0d:0E:0f", "-m", "src")
+    assert re.search(r"0a:0b:0c:0d:0e:0f\s+src\s", status(cli))
+    for bad in (("ip", "1.2.3"), ("ip", "zz::1"), ("ether", "aa:bb:cc:dd:ee"),
+                ("ether", "aa:bb:cc:dd:ee:fff"), ("port", "65536"), ("port", "80", "-m", "up")):
+        cli(*bad, ok=False)
+    cli("unload", "veth0")
+
+
+def test_map_capacity_overflow(cli):
+    # test_slow.py: the reference maps hold 10000 entries; the first address
+    # that does not fit is refused and must not be stored
+    cli("load", "veth0", "-f", "ipv4", "--capacity", 50)
+    for i in range(50):
+        cli("ip", f"10.1.0.{i}")
+    p = cli("ip", "10.1.1.1", ok=False)
+    assert "state map is full" in p.stderr
+    out = status(cli)
+    assert "10.1.1.1" not in out and out.count("10.1.0.") == 50
+    cli("ip", "10.1.0.7", "-r")                 # room again after a delete
+    cli("ip", "10.1.1.1")
+    cli("unload", "veth0")
+
+
+def test_poll(cli):
+    cli("load", "veth0")
+    p = cli("poll", "-i", 50, "-n", 2)
+    blocks = [b for b in p.stdout.split("\n\n") if b.strip()]
+    assert len(blocks) == 2
+    for b in blocks:
+        lines = b.splitlines()
+        assert lines[0].startswith("Period of ")
+        assert [l.split()[0] for l in lines[1:]] == ["XDP_DROP", "XDP_PASS", "XDP_TX",
+                                                     "XDP_REDIRECT"]
+    cli("poll", "-i", 0, ok=False)
+    cli("unload", "veth0")
+    p = cli("poll", "-n", 1, ok=False)
+    assert "Maybe xdp-filter is not loaded" in p.stderr
+
+
+def test_help_and_unknown(cli):
+    p = cli("help", ok=None)
+    assert "COMMAND can be one of" in p.stderr
+    cli("frobnicate", ok=False)
+    p = cli("port", "--help")
+    assert "--proto" in p.stderr

@@ -1,0 +1,203 @@
+"""GPU tests of the paths either side of the kernel:
+
+  * AF_XDP descriptor batches (xfg_classify_descs): a UMEM with 4 KiB frames,
+    aligned and unaligned-chunk addresses, an RX ring view that wraps;
+  * the CLI end to end: rules added with `xdp-filter ip/port/ether`, a pcap
+    classified with `xdp-filter run`, the pcapng verdict dump, and the hit
+    counters / stats that `status` then prints; the traffic checks of
+    xdp-filter/tests/test-xdp-filter.sh (ports allow/deny, :95-130) restated
+    as frames;
+  * the rule store's per-device reload.
+All bit-exact against the CPU restatement (oracle/) on the same frames.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import pcaputil as P
+import xftools as X
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+XF = os.path.join(ROOT, "xdp-tools_amd", "bin", "xdp-filter")
+
+
+@pytest.fixture(scope="module")
+def G():
+    import xfgpu
+    return xfgpu
+
+
+def test_classify_descs_umem_ring(G):
+    rules, pool = X.random_rules(61, n4=120, n6=60, ne=20, nports=30)
+    n = 20000
+    data, lens = X.gen_fuzz(23, n, 160, rules, pool)
+    feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    ov, orules, ost = X.run_oracle(feats, data, lens, rules, stride=160)
+    # UMEM: 4 KiB chunks; frame i in chunk perm[i] at headroom 256 (aligned
+    # mode) or, for every third frame, chunk base + offset in bits 48..63
+    # (unaligned-chunk mode)
+    rng = np.random.default_rng(4)
+    nchunks = n + 100
+    perm = rng.permutation(nchunks)[:n]
+    umem = np.zeros(nchunks * 4096, np.uint8)
+    addr = np.zeros(n, np.uint64)
+    for i in range(n):
+        base, head = int(perm[i]) * 4096, 256 + 16 * (i % 3)
+        umem[base + head:base + head + lens[i]] = data[i * 160:i * 160 + lens[i]]
+        addr[i] = (base | (head << 48)) if i % 3 == 2 else base + head
+    # RX ring of 32768 entries; the batch starts near the end so it wraps
+    ring, first = 32768, 32768 - 777
+    descs = np.zeros((ring, 2), np.uint64)
+    idx = (first + np.arange(n)) & (ring - 1)
+    descs[idx, 0] = addr
+    descs[idx, 1] = lens.astype(np.uint64)                  # len | options 0 << 32
+    f = G.Filter(feats, ndev=1)
+    f.load_rules(rules)
+    d_umem, d_descs, d_v = f.alloc(umem.nbytes), f.alloc(descs.nbytes), f.alloc(n)
+    d_umem.upload(umem)
+    d_descs.upload(descs)
+    f.classify_descs(d_umem.ptr, d_descs.ptr, n, d_v.ptr, first=first, mask=ring - 1)
+    f.sync()
+    v = d_v.download(np.zeros(n, np.uint8))
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(f.stats(), ost)
+    r = rules.prepared()
+    np.testing.assert_array_equal(f.values_of(G.MAP_IPV4, r.v4_keys), orules.v4_vals)
+    np.testing.assert_array_equal(f.values_of(G.MAP_PORTS, np.arange(65536, dtype=np.uint32)),
+                                  orules.ports)
+    with pytest.raises(OSError):      # a ring mask must be 2^k - 1
+        f.classify_descs(d_umem.ptr, d_descs.ptr, n, d_v.ptr, mask=1000)
+    f.close()
+
+
+def test_store_reload_keeps_counters(G, tmp_path):
+    d = str(tmp_path)
+    rules, pool = X.random_rules(71, n4=100, n6=40, ne=10, nports=20)
+    data, lens = X.gen_fuzz(3, 30000, 160, rules, pool)
+    feats = X.VARIANT_FEATURES["xdpfilt_alw_all"]
+    for m in range(4):
+        G.lib.xfg_store_create_map(d.encode(), m, 10000)
+    f = G.Filter(feats, ndev=1)
+    f.load_rules(rules)
+    f.run(data, lens, stride=160)
+    f.store_save(d)
+    f.close()
+    f = G.Filter(feats, ndev=1)
+    f.store_load(d)
+    f.run(data, lens, stride=160)
+    _, once, _ = X.run_oracle(feats, data, lens, rules, stride=160)
+    _, twice, _ = X.run_oracle(feats, data, lens, once, stride=160)
+    r = rules.prepared()
+    np.testing.assert_array_equal(f.values_of(G.MAP_IPV6, r.v6_keys), twice.v6_vals)
+    np.testing.assert_array_equal(f.values_of(G.MAP_PORTS, np.arange(65536, dtype=np.uint32)),
+                                  twice.ports)
+    f.close()
+
+
+@pytest.fixture
+def cli(tmp_path):
+    env = dict(os.environ, XDP_FILTER_STATE_DIR=str(tmp_path / "state"))
+
+    def run(*args, ok=True):
+        p = subprocess.run([XF, *map(str, args)], env=env, capture_output=True, text=True,
+                           timeout=120)
+        if ok:
+            assert p.returncode == 0, (args, p.stdout, p.stderr)
+        return p
+    return run
+
+
+def _parse_status(out):
+    """{key: (flags, hits)} of every Filtered ... section, and the stats."""
+    rules, stats = {}, {}
+    for line in out.splitlines():
+        m = re.fullmatch(r"  (XDP_\w+)\s+(\d+) pkts\s+(\d+) KiB", line)
+        if m:
+            stats[m.group(1)] = int(m.group(2))
+            continue
+        m = re.fullmatch(r"  (\S+)\s+([a-z,]+)\s+(\d+)", line)
+        if m and m.group(1) != "Mode":
+            rules[m.group(1)] = (m.group(2), int(m.group(3)))
+    return rules, stats
+
+
+def test_cli_run_end_to_end(G, cli, tmp_path):
+    # rules through the CLI, traffic from a pcap, verdicts through the dump
+    import ipaddress
+    rs, pool = X.random_rules(81, n4=40, n6=20, ne=8, nports=12, flag_mode="dst")
+    cli("load", "veth0", "-p", "deny")
+    for k in rs.v4_keys:
+        cli("ip", str(ipaddress.IPv4Address(bytes(k))))
+    for k in rs.v6_keys:
+        cli("ip", str(ipaddress.IPv6Address(bytes(k))))
+    for k in rs.eth_keys:
+        cli("ether", ":".join(f"{b:02x}" for b in k))
+    for p in pool:
+        cli("port", int(p))
+    # what the CLI stored, as oracle rules: ip/ether dst, ports dst,tcp,udp
+    rules = X.RuleSet()
+    rules.v4_keys, rules.v6_keys, rules.eth_keys = rs.v4_keys, rs.v6_keys, rs.eth_keys
+    rules.v4_vals = np.full(len(rs.v4_keys), 2, np.uint64)
+    rules.v6_vals = np.full(len(rs.v6_keys), 2, np.uint64)
+    rules.eth_vals = np.full(len(rs.eth_keys), 2, np.uint64)
+    for p in pool:
+        rules.ports[X.port_key(int(p))] = 2 | 4 | 8
+    data, lens = X.gen_fuzz(17, 5000, 160, rules, pool)
+    frames = P.frames_of(data, lens, stride=160)
+    pcap = tmp_path / "in.pcap"
+    P.write_pcap(pcap, frames)
+    bdata, boffs, blens = P.batch_from(frames)
+    feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    ov, orules, ost = X.run_oracle(feats, bdata, blens, rules, offsets=boffs)
+    dump = tmp_path / "out.pcapng"
+    out = cli("run", "veth0", pcap, "--dump", dump).stdout
+    assert "Classified 5000 packets on veth0 with xdpfilt_dny_all" in out
+    got = P.read_verdict_pcapng(dump)
+    assert [g[0] for g in got] == frames
+    np.testing.assert_array_equal([g[2] for g in got], ov)
+    st_rules, stats = _parse_status(cli("status").stdout)
+    assert stats == {"XDP_ABORTED": int(ost[0, 0]), "XDP_DROP": int(ost[1, 0]),
+                     "XDP_PASS": int(ost[2, 0])}
+    for k, v in zip(rs.v4_keys, orules.v4_vals):
+        assert st_rules[str(ipaddress.IPv4Address(bytes(k)))] == ("dst", int(v) >> 6)
+    for p in pool:
+        assert st_rules[str(int(p))] == ("dst,tcp,udp", int(orules.ports[X.port_key(int(p))]) >> 6)
+    # a second run accumulates, like packets arriving later
+    cli("run", "veth0", pcap, "-q")
+    st2, stats2 = _parse_status(cli("status").stdout)
+    assert stats2["XDP_PASS"] == 2 * stats["XDP_PASS"]
+    cli("unload", "veth0")
+
+
+@pytest.mark.parametrize("policy", ["allow", "deny"])
+def test_cli_ports_traffic(G, cli, tmp_path, policy):
+    # test-xdp-filter.sh:95-130: TCP/UDP to port 10000 vs 10001 before, while
+    # and after port 10000 is filtered
+    def frame(proto, dport):
+        eth = bytes.fromhex("02000000000102000000000286dd")
+        l4 = (bytes.fromhex("c0de") + dport.to_bytes(2, "big") +
+              (bytes(8) + bytes([0x50, 0x02]) + bytes(6) if proto == 6 else bytes([0, 13, 0, 0])))
+        ip6 = bytes([0x60, 0, 0, 0]) + len(l4 + b"x").to_bytes(2, "big") + bytes([proto, 64]) + \
+            bytes(15) + b"\x01" + bytes(15) + b"\x02"
+        return eth + ip6 + l4 + b"x"
+    frames = [frame(6, 10000), frame(17, 10000), frame(6, 10001), frame(17, 10001)]
+    pcap = tmp_path / "p.pcap"
+    P.write_pcap(pcap, frames)
+    PASS, DROP = 2, 1
+    ok, blocked = (PASS, DROP) if policy == "allow" else (DROP, PASS)
+    cli("load", "veth0", "-p", policy, "-f", "udp,tcp")
+
+    def verdicts():
+        cli("run", "veth0", pcap, "-d", tmp_path / "v.pcapng", "-q")
+        return [g[2] for g in P.read_verdict_pcapng(tmp_path / "v.pcapng")]
+    assert verdicts() == [ok] * 4
+    cli("port", 10000)
+    assert verdicts() == [blocked, blocked, ok, ok]
+    cli("port", 10000, "-r")
+    assert verdicts() == [ok] * 4
+    cli("unload", "veth0")

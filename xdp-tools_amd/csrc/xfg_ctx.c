@@ -1059,6 +1059,39 @@ int xfg_classify(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verd
 	return err;
 }
 
+int xfg_classify_descs(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *db,
+		       uint8_t *verdicts, void *stream)
+{
+	if (!ctx || !db || (!verdicts && db->count))
+		return -EINVAL;
+	if (!ctx->ndev)
+		return -ENODEV;
+	if (dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	if (!db->count)
+		return 0;
+	if (!db->umem || !db->descs || ((uintptr_t)db->descs & 7) || (db->mask & (db->mask + 1u)))
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[dev];
+	struct xfg_batch b = { db->umem, NULL, NULL, db->count, 0, 0 };
+	struct xfg_kargs a;
+	pthread_mutex_lock(&ctx->lock);
+	ctx->reduced = 0;
+	int err = fill_kargs(ctx, d, &b, verdicts, &a);
+	pthread_mutex_unlock(&ctx->lock);
+	if (err)
+		return err;
+	a.descs = db->descs;
+	a.desc_mask = db->mask;
+	a.desc_first = db->first;
+	a.window = 128;
+	a.streamed = 0;
+	err = hip_err(hipSetDevice(d->ordinal));
+	if (!err)
+		err = launch_batch(ctx, d, &a, stream, 1);
+	return err;
+}
+
 int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verdicts,
 		       int iters, double *avg_ms)
 {

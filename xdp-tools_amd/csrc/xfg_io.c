@@ -713,8 +713,8 @@ int xfg_store_save(xfg_ctx *ctx, const char *dir)
 			continue;   /* not pinned: this program does not use the map */
 		if (err)
 			return err;
-		uint8_t *keys;
-		uint64_t *vals, n;
+		uint8_t *keys = NULL;
+		uint64_t *vals = NULL, n = 0;
 		if ((err = collect(ctx, map, &keys, &vals, &n)))
 			return err;
 		err = write_map(dir, map, h.capacity, keys, vals, n);

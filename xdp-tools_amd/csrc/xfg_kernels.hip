@@ -734,14 +734,28 @@ struct Stamps {
 	}
 };
 
+// Word w of packet i's AF_XDP descriptor (ring index wraps with desc_mask).
+__device__ __forceinline__ uint64_t desc_word(const xfg_kargs &a, uint64_t i, int w)
+{
+	return a.descs[2ull * ((a.desc_first + (uint32_t)i) & a.desc_mask) + w];
+}
+
 __device__ __forceinline__ uint32_t load_len(const xfg_kargs &a, uint64_t i)
 {
+	if (a.descs)
+		return (uint32_t)desc_word(a, i, 1);   // xdp_desc.len (low half, little-endian)
 	return a.lens_u16 ? static_cast<const uint16_t *>(a.lens)[i]
 			  : static_cast<const uint32_t *>(a.lens)[i];
 }
 
 __device__ __forceinline__ const uint8_t *pkt_ptr(const xfg_kargs &a, uint64_t i)
 {
+	if (a.descs) {
+		// xsk_umem__add_offset_to_addr() (headers/xdp/xsk.h:173-186): the
+		// unaligned-chunk mode keeps an offset in bits 48..63
+		const uint64_t addr = desc_word(a, i, 0);
+		return a.data + (addr & ((1ull << 48) - 1)) + (addr >> 48);
+	}
 	return a.data + (a.offsets ? a.offsets[i] : i * (uint64_t)a.stride);
 }
 

@@ -112,6 +112,13 @@ struct xfg_kargs {
 	 * v6 slots, eth slots (each with its zero-key slot), then the 65536
 	 * ports; gbase[i] = first index of each. */
 	uint32_t gbase[4];
+	/* AF_XDP descriptors (xfg_classify_descs): packet i is record
+	 * (desc_first + i) & desc_mask of an array of struct xdp_desc {u64 addr;
+	 * u32 len; u32 options} (headers/linux/if_xdp.h:110-114) over the UMEM at
+	 * `data`; NULL for the other layouts */
+	const uint64_t *descs;
+	uint32_t desc_mask;
+	uint32_t desc_first;
 };
 
 

@@ -43,7 +43,15 @@ EXPORTS = [
     "xfg_classify_host", "xfg_stats_read", "xfg_stats_read_dev", "xfg_stats_reset",
     "xfg_sync", "xfg_dev_alloc", "xfg_dev_free", "xfg_memcpy_h2d", "xfg_memcpy_d2h",
     "xfg_host_alloc_pinned", "xfg_host_free_pinned", "xfg_classify_timed", "xfg_stream_read_timed",
-    "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce",
+    "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce", "xfg_map_update_batch_percpu",
+    "xfg_classify_descs",
+]
+# include/xdpfilter_io.h
+IO_EXPORTS = [
+    "xfg_pcap_read", "xfg_host_batch_free", "xfg_pcapng_write_verdicts", "xfg_store_map_name",
+    "xfg_store_has_map", "xfg_store_create_map", "xfg_store_remove_map", "xfg_store_map_capacity",
+    "xfg_store_load", "xfg_store_save", "xfg_store_stats_read", "xfg_store_stats_write",
+    "xfg_store_stats_remove",
 ]
 
 
@@ -61,6 +69,18 @@ class Batch(C.Structure):
 
 class StatsRecord(C.Structure):
     _fields_ = [("packets", C.c_uint64), ("bytes", C.c_uint64)]
+
+
+class DescBatch(C.Structure):
+    _fields_ = [("umem", C.c_void_p), ("descs", C.c_void_p), ("first", C.c_uint32),
+                ("mask", C.c_uint32), ("count", C.c_uint64)]
+
+
+class HostBatch(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offsets", C.POINTER(C.c_uint64)),
+                ("lens", C.POINTER(C.c_uint32)), ("orig_lens", C.POINTER(C.c_uint32)),
+                ("ts_ns", C.POINTER(C.c_uint64)), ("count", C.c_uint64), ("bytes", C.c_uint64),
+                ("linktype", C.c_uint32), ("pad", C.c_uint32)]
 
 
 def _load():
@@ -82,10 +102,26 @@ def _load():
         "xfg_map_get_next_key": (C.c_int, [vp, C.c_int, vp, vp]),
         "xfg_map_count": (C.c_int64, [vp, C.c_int]),
         "xfg_map_update_batch": (C.c_int, [vp, C.c_int, vp, u64p, C.c_uint64]),
+        "xfg_map_update_batch_percpu": (C.c_int, [vp, C.c_int, vp, u64p, C.c_uint64]),
+        "xfg_pcap_read": (C.c_int, [C.c_char_p, C.POINTER(HostBatch)]),
+        "xfg_host_batch_free": (None, [C.POINTER(HostBatch)]),
+        "xfg_pcapng_write_verdicts": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(HostBatch),
+                                                C.POINTER(C.c_uint8)]),
+        "xfg_store_map_name": (C.c_char_p, [C.c_int]),
+        "xfg_store_has_map": (C.c_int, [C.c_char_p, C.c_int]),
+        "xfg_store_create_map": (C.c_int, [C.c_char_p, C.c_int, C.c_uint32]),
+        "xfg_store_remove_map": (C.c_int, [C.c_char_p, C.c_int]),
+        "xfg_store_map_capacity": (C.c_int64, [C.c_char_p, C.c_int]),
+        "xfg_store_load": (C.c_int, [vp, C.c_char_p]),
+        "xfg_store_save": (C.c_int, [vp, C.c_char_p]),
+        "xfg_store_stats_read": (C.c_int, [C.c_char_p, C.POINTER(StatsRecord)]),
+        "xfg_store_stats_write": (C.c_int, [C.c_char_p, C.POINTER(StatsRecord)]),
+        "xfg_store_stats_remove": (C.c_int, [C.c_char_p]),
         "xfg_map_lookup_batch": (C.c_int64, [vp, C.c_int, vp, C.c_uint64, u64p,
                                              C.POINTER(C.c_uint8)]),
         "xfg_classify": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, vp]),
         "xfg_classify_host": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp]),
+        "xfg_classify_descs": (C.c_int, [vp, C.c_int, C.POINTER(DescBatch), vp, vp]),
         "xfg_classify_timed": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, C.c_int,
                                          C.POINTER(C.c_double)]),
         "xfg_stream_read_timed": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_int,
@@ -125,6 +161,46 @@ def select_program(features: int):
     feats = C.c_uint32()
     _check(lib.xfg_select_program(features, C.byref(name), C.byref(feats)), "select_program")
     return name.value.decode(), feats.value
+
+
+def read_pcap(path):
+    """pcap / pcapng file -> (data u8, offsets u64, lens u32, orig_lens u32, ts_ns u64),
+    frames at 16-byte aligned offsets (xfg_pcap_read)."""
+    hb = HostBatch()
+    _check(lib.xfg_pcap_read(os.fsencode(path), C.byref(hb)), "pcap_read")
+    try:
+        n = hb.count
+        data = np.ctypeslib.as_array((C.c_uint8 * max(hb.bytes + 16, 16)).from_address(hb.data)).copy()
+        out = [data]
+        for ptr_, dt in ((hb.offsets, np.uint64), (hb.lens, np.uint32), (hb.orig_lens, np.uint32),
+                         (hb.ts_ns, np.uint64)):
+            out.append(np.ctypeslib.as_array(ptr_, shape=(n,)).astype(dt) if n else np.zeros(0, dt))
+        return tuple(out)
+    finally:
+        lib.xfg_host_batch_free(C.byref(hb))
+
+
+def write_verdicts_pcapng(path, ifname, data, offsets, lens, verdicts, orig_lens=None, ts_ns=None):
+    """pcapng dump with the EPB verdict option (xfg_pcapng_write_verdicts)."""
+    n = len(lens)
+    data = np.ascontiguousarray(data, np.uint8)
+    offs = np.ascontiguousarray(offsets, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    ol = np.ascontiguousarray(orig_lens if orig_lens is not None else lens, np.uint32)
+    ts = np.ascontiguousarray(ts_ns if ts_ns is not None else np.zeros(n), np.uint64)
+    v = np.ascontiguousarray(verdicts, np.uint8)
+    hb = HostBatch(data.ctypes.data, offs.ctypes.data_as(C.POINTER(C.c_uint64)),
+                   lens.ctypes.data_as(C.POINTER(C.c_uint32)),
+                   ol.ctypes.data_as(C.POINTER(C.c_uint32)),
+                   ts.ctypes.data_as(C.POINTER(C.c_uint64)), n, data.nbytes, 1, 0)
+    _check(lib.xfg_pcapng_write_verdicts(os.fsencode(path), ifname.encode(), C.byref(hb),
+                                         v.ctypes.data_as(C.POINTER(C.c_uint8))), "pcapng_write")
+
+
+def store_stats(state_dir):
+    recs = (StatsRecord * ACTION_MAX)()
+    _check(lib.xfg_store_stats_read(os.fsencode(state_dir), recs), "store_stats_read")
+    return np.array([[r.packets, r.bytes] for r in recs], np.uint64)
 
 
 def _key_buf(map_id, key) -> C.Array:
@@ -245,6 +321,21 @@ class Filter:
     def count(self, map_id):
         return _check(lib.xfg_map_count(self.ctx, map_id), "count")
 
+    def update_batch_percpu(self, map_id, keys: np.ndarray, vals: np.ndarray):
+        """vals[n, nvals]: one value per device, as bpf_map_update_elem on a per-CPU map."""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        vals = np.ascontiguousarray(vals, np.uint64)
+        assert vals.ndim == 2 and vals.shape[1] == self.nvals
+        _check(lib.xfg_map_update_batch_percpu(self.ctx, map_id, keys.ctypes.data,
+                                               vals.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                               len(vals)), "update_batch_percpu")
+
+    def store_load(self, state_dir):
+        _check(lib.xfg_store_load(self.ctx, os.fsencode(state_dir)), "store_load")
+
+    def store_save(self, state_dir):
+        _check(lib.xfg_store_save(self.ctx, os.fsencode(state_dir)), "store_save")
+
     def update_batch(self, map_id, keys: np.ndarray, vals: np.ndarray):
         keys = np.ascontiguousarray(keys, np.uint8)
         vals = np.ascontiguousarray(vals, np.uint64)
@@ -296,6 +387,12 @@ class Filter:
                  lens_u16=False, dev=0, stream=None):
         b = Batch(data_ptr, offsets_ptr, lens_ptr, count, stride, int(lens_u16))
         _check(lib.xfg_classify(self.ctx, dev, C.byref(b), verdicts_ptr, stream), "classify")
+
+    def classify_descs(self, umem_ptr, descs_ptr, count, verdicts_ptr, first=0, mask=0xffffffff,
+                       dev=0, stream=None):
+        b = DescBatch(umem_ptr, descs_ptr, first, mask, count)
+        _check(lib.xfg_classify_descs(self.ctx, dev, C.byref(b), verdicts_ptr, stream),
+               "classify_descs")
 
     def classify_timed(self, data_ptr, lens_ptr, count, stride, verdicts_ptr, iters,
                        offsets_ptr=None, lens_u16=False, dev=0):
