@@ -978,6 +978,7 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 			a->port_count = 0;
 		}
 	}
+	a->dense = !a->offsets && !a->descs && a->stride == a->window;
 	return 0;
 }
 
@@ -1086,6 +1087,7 @@ int xfg_classify_descs(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *db,
 	a.desc_first = db->first;
 	a.window = 128;
 	a.streamed = 0;
+	a.dense = 0;
 	err = hip_err(hipSetDevice(d->ordinal));
 	if (!err)
 		err = launch_batch(ctx, d, &a, stream, 1);

@@ -65,6 +65,7 @@
 
 #define XFG_BLOOM_K       4u
 
+
 /* Per-hash-map descriptor passed to the kernel by value. */
 struct xfg_tdesc {
 	const void *buckets;         /* (nbuckets + 1) * 64 B */
@@ -119,6 +120,7 @@ struct xfg_kargs {
 	const uint64_t *descs;
 	uint32_t desc_mask;
 	uint32_t desc_first;
+	uint32_t dense;               /* stride == window, no offsets/descriptors */
 };
 
 
