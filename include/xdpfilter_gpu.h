@@ -193,6 +193,18 @@ int xfg_classify_descs(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *batch
 int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
 		      uint8_t *verdicts);
 
+/*
+ * Verdict compaction: writes the indices i (ascending) with verdicts[i] ==
+ * @action to @idx and their number to *@count — the list a forwarding stage
+ * walks (the reference passes XDP_PASS frames on up the chain,
+ * xdp-filter/xdpfilt_prog.h:209-212).  Device memory: @verdicts (n bytes),
+ * @idx (room for n u32), @count (one u64).  One pass (wave ballots and
+ * prefix sums, decoupled look-back between tiles), stream-ordered on @stream
+ * (NULL: the library's stream of the device).  n < 2^32.
+ */
+int xfg_compact(xfg_ctx *ctx, int dev, const uint8_t *verdicts, uint64_t n, uint32_t action,
+		uint32_t *idx, uint64_t *count, void *stream);
+
 /* Per-action stats summed over devices (the userspace per-CPU sum of
  * lib/util/stats.c:140-172), or for one device. */
 int xfg_stats_read(xfg_ctx *ctx, struct xfg_stats_record out[XFG_ACTION_MAX]);

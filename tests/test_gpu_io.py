@@ -201,3 +201,48 @@ def test_cli_ports_traffic(G, cli, tmp_path, policy):
     cli("port", 10000, "-r")
     assert verdicts() == [ok] * 4
     cli("unload", "veth0")
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 4095, 4096, 4097, 65536 * 3 + 7, (1 << 22) + 13])
+def test_compact_matches_nonzero(G, n):
+    """Ordered verdict compaction (xfg_compact) equals np.nonzero for every
+    action, on tile-boundary and ragged sizes."""
+    rng = np.random.default_rng(n)
+    v = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.05, 0.45, 0.5]).astype(np.uint8)
+    f = G.Filter(X.VARIANT_FEATURES["xdpfilt_dny_all"], ndev=1)
+    d_v, d_i, d_c = f.alloc(max(n, 16)), f.alloc(max(4 * n, 16)), f.alloc(16)
+    if n:
+        d_v.upload(v)
+    for action in (0, 1, 2, 3):
+        f.compact(d_v.ptr, n, action, d_i.ptr, d_c.ptr)
+        f.sync()
+        cnt = int(d_c.download(np.zeros(1, np.uint64))[0])
+        want = np.nonzero(v == action)[0].astype(np.uint32)
+        assert cnt == len(want)
+        if cnt:
+            np.testing.assert_array_equal(d_i.download(np.zeros(cnt, np.uint32)), want)
+    f.close()
+
+
+def test_compact_pass_list_after_classify(G):
+    """The PASS list of a classified C3 batch, as a forwarding stage uses it."""
+    n = 1 << 20
+    v4 = X.rand_keys(3, 50000, 4)
+    data, lens = X.gen_workload(3, 3, n, 64, v4=v4)
+    rules = X.RuleSet()
+    rules.v4_keys, rules.v4_vals = v4, np.full(len(v4), 2, np.uint64)
+    ov, _, _ = X.run_oracle(X.VARIANT_FEATURES["xdpfilt_dny_all"], data, lens, rules, stride=64,
+                            nthreads=8)
+    f = G.Filter(X.VARIANT_FEATURES["xdpfilt_dny_all"], ndev=1, ipv4_capacity=len(v4))
+    f.load_rules(rules)
+    d_data, d_lens, d_v = f.alloc(data.nbytes), f.alloc(lens.nbytes), f.alloc(n)
+    d_i, d_c = f.alloc(4 * n), f.alloc(16)
+    d_data.upload(data)
+    d_lens.upload(lens)
+    f.classify(d_data.ptr, d_lens.ptr, n, 64, d_v.ptr)
+    f.compact(d_v.ptr, n, 2, d_i.ptr, d_c.ptr)
+    f.sync()
+    cnt = int(d_c.download(np.zeros(1, np.uint64))[0])
+    np.testing.assert_array_equal(d_i.download(np.zeros(cnt, np.uint32)),
+                                  np.nonzero(ov == 2)[0].astype(np.uint32))
+    f.close()

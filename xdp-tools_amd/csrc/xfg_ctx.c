@@ -32,6 +32,10 @@ int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a, unsig
 int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sink, unsigned grid,
 			   void *stream);
 int xfg_classify_occupancy(uint32_t prog_features, uint32_t window);
+int xfg_launch_compact(const uint8_t *verdicts, uint64_t n, uint32_t action, uint32_t *idx,
+		       unsigned long long *count, unsigned long long *status, uint32_t *ticket,
+		       unsigned grid, void *stream);
+uint64_t xfg_compact_tiles(uint64_t n);
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
 #define PORT_BITS_WORDS (XFG_PORT_MAP_ENTRIES / 32)
@@ -64,6 +68,9 @@ struct xfg_dev {
 	uint32_t port_tab_disp;
 	int port_tab_ok, port_tab_dirty;
 	int occ64, occ128, occ_st;      /* resident classify workgroups per CU */
+	unsigned long long *cstatus;    /* verdict compaction: tile status words */
+	uint64_t cstatus_cap;
+	uint32_t *cticket;
 	hipEvent_t ev_user, ev_done;    /* ordering against a caller's stream */
 };
 
@@ -182,6 +189,8 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->prof);
 	hipFree(d->port_tab);
 	free(d->port_flags_h);
+	hipFree(d->cstatus);
+	hipFree(d->cticket);
 	if (d->ev_user)
 		hipEventDestroy(d->ev_user);
 	if (d->ev_done)
@@ -1121,6 +1130,38 @@ int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t
 	*avg_ms = ms / iters;
 	return 0;
 fail:
+	return err;
+}
+
+/* Verdict compaction (include/xdpfilter_gpu.h). */
+int xfg_compact(xfg_ctx *ctx, int dev, const uint8_t *verdicts, uint64_t n, uint32_t action,
+		uint32_t *idx, uint64_t *count, void *stream)
+{
+	int err = 0;
+	if (!ctx || !count || (n && (!verdicts || !idx)) || action > 255 || n > 0xffffffffull)
+		return -EINVAL;
+	if (!ctx->ndev)
+		return -ENODEV;
+	if (dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	struct xfg_dev *d = &ctx->dev[dev];
+	uint64_t tiles = xfg_compact_tiles(n);
+	pthread_mutex_lock(&ctx->lock);
+	HIPCHK(hipSetDevice(d->ordinal));
+	if (!d->cticket)
+		HIPCHK(hipMalloc((void **)&d->cticket, 4));
+	if (tiles > d->cstatus_cap) {
+		hipFree(d->cstatus);
+		d->cstatus = NULL;
+		d->cstatus_cap = 0;
+		HIPCHK(hipMalloc((void **)&d->cstatus, tiles * 8));
+		d->cstatus_cap = tiles;
+	}
+	hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+	err = xfg_launch_compact(verdicts, n, action, idx, (unsigned long long *)count,
+				 d->cstatus, d->cticket, (unsigned)d->ncu * 4, s);
+fail:
+	pthread_mutex_unlock(&ctx->lock);
 	return err;
 }
 

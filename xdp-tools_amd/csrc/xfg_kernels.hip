@@ -1509,3 +1509,150 @@ extern "C" int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sin
 			   bytes / 16, static_cast<u32x4 *>(sink));
 	return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+// ---------------------------------------------------------------- verdict compaction
+// The indices of the packets whose verdict equals `action`, in packet order
+// (the PASS list a forwarding stage walks: the reference chains only on
+// XDP_PASS, xdp-filter/xdpfilt_prog.h:209-212).  One pass over the verdict
+// bytes: a workgroup takes tiles of CT_TILE verdicts in ticket order; each
+// lane counts its 16 bytes, wave prefix sums (shuffles) and an LDS step give
+// the workgroup's offsets, and a decoupled look-back over the earlier tiles'
+// published {flag, sum} words gives the tile's base.  A status word packs
+// flag (bits 62-63: 1 = tile aggregate, 2 = inclusive prefix) and value, so
+// one 8-byte agent-scope atomic carries both.
+namespace {
+constexpr int CT_LANES = 256;
+constexpr int CT_TILE = CT_LANES * 16;
+constexpr unsigned long long CT_AGG = 1ull << 62, CT_INC = 2ull << 62, CT_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint32_t count_eq(uint32_t w, uint32_t act4)
+{
+	const uint32_t x = w ^ act4;   // a zero byte where the verdict matches
+	const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+	return __builtin_popcount(z);
+}
+}  // namespace
+
+__global__ __launch_bounds__(CT_LANES) void xfg_compact_kernel(
+	const uint8_t *__restrict__ verdicts, uint64_t n, uint32_t action,
+	uint32_t *__restrict__ idx, unsigned long long *__restrict__ count,
+	unsigned long long *status, uint32_t *ticket, uint64_t ntiles)
+{
+	__shared__ uint32_t s_wave[CT_LANES / 64];
+	__shared__ uint64_t s_tile, s_base;
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const uint32_t act4 = action * 0x01010101u;
+	for (;;) {
+		if (tid == 0)
+			s_tile = atomicAdd(ticket, 1u);
+		__syncthreads();
+		const uint64_t t = s_tile;
+		if (t >= ntiles)
+			break;
+		const uint64_t first = t * CT_TILE + (uint64_t)tid * 16;
+		uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+		uint32_t valid = 0;   // bytes of this lane inside the batch
+		if (first + 16 <= n) {
+			const u32x4 v = __builtin_nontemporal_load(
+				reinterpret_cast<const u32x4 *>(verdicts + first));
+			w0 = v.x;
+			w1 = v.y;
+			w2 = v.z;
+			w3 = v.w;
+			valid = 16;
+		} else if (first < n) {
+			valid = (uint32_t)(n - first);
+		}
+		auto byte_at = [&](uint32_t k) -> uint32_t {
+			if (valid < 16)   // the batch's last lane: read the tail bytewise
+				return verdicts[first + k];
+			const uint32_t w = k < 4 ? w0 : k < 8 ? w1 : k < 12 ? w2 : w3;
+			return (w >> (8 * (k & 3))) & 0xff;
+		};
+		uint32_t mine = 0;
+		if (valid == 16) {
+			mine = count_eq(w0, act4) + count_eq(w1, act4) + count_eq(w2, act4) +
+			       count_eq(w3, act4);
+		} else {
+			for (uint32_t k = 0; k < valid; k++)
+				mine += byte_at(k) == action;
+		}
+		// wave inclusive scan, then the workgroup's
+		uint32_t x = mine;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t y = __shfl_up(x, o);
+			if (lane >= o)
+				x += y;
+		}
+		if (lane == 63)
+			s_wave[wave] = x;
+		__syncthreads();
+		uint32_t before = x - mine, agg = 0;
+#pragma unroll
+		for (int k = 0; k < CT_LANES / 64; k++) {
+			before += k < wave ? s_wave[k] : 0;
+			agg += s_wave[k];
+		}
+		// decoupled look-back (one lane): publish the aggregate, walk back
+		if (tid == 0) {
+			unsigned long long base = 0;
+			if (t == 0) {
+				__hip_atomic_store(&status[0], CT_INC | agg, __ATOMIC_RELAXED,
+						   __HIP_MEMORY_SCOPE_AGENT);
+			} else {
+				__hip_atomic_store(&status[t], CT_AGG | agg, __ATOMIC_RELAXED,
+						   __HIP_MEMORY_SCOPE_AGENT);
+				for (uint64_t p = t - 1;;) {
+					const unsigned long long w = __hip_atomic_load(
+						&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					if (w & CT_INC) {
+						base += w & CT_VAL;
+						break;
+					}
+					if (w & CT_AGG) {
+						base += w & CT_VAL;
+						p--;   // tile 0 always publishes CT_INC
+						continue;
+					}
+					__builtin_amdgcn_s_sleep(1);   // predecessor still counting
+				}
+				__hip_atomic_store(&status[t], CT_INC | (base + agg), __ATOMIC_RELAXED,
+						   __HIP_MEMORY_SCOPE_AGENT);
+			}
+			s_base = base;
+			if (t == ntiles - 1)
+				*count = base + agg;
+		}
+		__syncthreads();
+		uint64_t pos = s_base + before;
+		if (mine) {
+			for (uint32_t k = 0; k < valid; k++)
+				if (byte_at(k) == action)
+					idx[pos++] = (uint32_t)(first + k);
+		}
+		__syncthreads();   // s_tile / s_wave reuse
+	}
+}
+
+extern "C" int xfg_launch_compact(const uint8_t *verdicts, uint64_t n, uint32_t action,
+				  uint32_t *idx, unsigned long long *count,
+				  unsigned long long *status, uint32_t *ticket, unsigned grid,
+				  void *stream)
+{
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	const uint64_t ntiles = (n + CT_TILE - 1) / CT_TILE;
+	if (hipMemsetAsync(status, 0, ntiles * 8, s) != hipSuccess ||
+	    hipMemsetAsync(ticket, 0, 4, s) != hipSuccess)
+		return -5;
+	if (!n)
+		return hipMemsetAsync(count, 0, 8, s) == hipSuccess ? 0 : -5;
+	hipLaunchKernelGGL(xfg_compact_kernel, dim3(grid), dim3(CT_LANES), 0, s, verdicts, n, action,
+			   idx, count, status, ticket, ntiles);
+	return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" uint64_t xfg_compact_tiles(uint64_t n)
+{
+	return (n + CT_TILE - 1) / CT_TILE;
+}

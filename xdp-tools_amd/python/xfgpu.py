@@ -44,7 +44,7 @@ EXPORTS = [
     "xfg_sync", "xfg_dev_alloc", "xfg_dev_free", "xfg_memcpy_h2d", "xfg_memcpy_d2h",
     "xfg_host_alloc_pinned", "xfg_host_free_pinned", "xfg_classify_timed", "xfg_stream_read_timed",
     "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce", "xfg_map_update_batch_percpu",
-    "xfg_classify_descs",
+    "xfg_classify_descs", "xfg_compact",
 ]
 # include/xdpfilter_io.h
 IO_EXPORTS = [
@@ -122,6 +122,7 @@ def _load():
         "xfg_classify": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, vp]),
         "xfg_classify_host": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp]),
         "xfg_classify_descs": (C.c_int, [vp, C.c_int, C.POINTER(DescBatch), vp, vp]),
+        "xfg_compact": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
         "xfg_classify_timed": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, C.c_int,
                                          C.POINTER(C.c_double)]),
         "xfg_stream_read_timed": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_int,
@@ -393,6 +394,10 @@ class Filter:
         b = DescBatch(umem_ptr, descs_ptr, first, mask, count)
         _check(lib.xfg_classify_descs(self.ctx, dev, C.byref(b), verdicts_ptr, stream),
                "classify_descs")
+
+    def compact(self, verdicts_ptr, n, action, idx_ptr, count_ptr, dev=0, stream=None):
+        _check(lib.xfg_compact(self.ctx, dev, verdicts_ptr, n, action, idx_ptr, count_ptr, stream),
+               "compact")
 
     def classify_timed(self, data_ptr, lens_ptr, count, stride, verdicts_ptr, iters,
                        offsets_ptr=None, lens_u16=False, dev=0):
