@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "xdp-tools_amd", "python"))
 
 import bench  # noqa: E402
 
-KNOBS = ("XFG_ABLATE", "XFG_VARIANT", "XFG_GRID_PER_CU", "XFG_KERNEL")
+KNOBS = ("XFG_ABLATE", "XFG_VARIANT", "XFG_GRID_PER_CU", "XFG_KERNEL", "XFG_COUNT", "XFG_SPEC")
 
 
 def main():

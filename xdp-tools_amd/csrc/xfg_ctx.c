@@ -68,6 +68,15 @@ struct xfg_dev {
 	uint32_t port_tab_disp;
 	int port_tab_ok, port_tab_dirty;
 	int occ64, occ128, occ_st;      /* resident classify workgroups per CU */
+	int occ_p64, occ_p128;          /* the same for the pipelined kernel */
+	int occ_s64;                    /* the speculative kernel (64-byte window) */
+	void *slog;                     /* speculative records */
+	uint32_t *slog_cnt;
+	uint64_t slog_bytes, slog_cnt_bytes;
+	uint32_t *fix;                  /* pipelined kernel: deferred-packet lists */
+	uint64_t fix_bytes;
+	uint32_t *hlog, *hlog_cnt;      /* pipelined kernel: hit log */
+	uint64_t hlog_bytes, hlog_cnt_bytes;
 	unsigned long long *cstatus;    /* verdict compaction: tile status words */
 	uint64_t cstatus_cap;
 	uint32_t *cticket;
@@ -190,6 +199,11 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->port_tab);
 	free(d->port_flags_h);
 	hipFree(d->cstatus);
+	hipFree(d->fix);
+	hipFree(d->hlog);
+	hipFree(d->hlog_cnt);
+	hipFree(d->slog);
+	hipFree(d->slog_cnt);
 	hipFree(d->cticket);
 	if (d->ev_user)
 		hipEventDestroy(d->ev_user);
@@ -247,6 +261,9 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	d->occ64 = xfg_classify_occupancy(ctx->prog_features, 64);
 	d->occ128 = xfg_classify_occupancy(ctx->prog_features, 128);
 	d->occ_st = xfg_classify_occupancy(ctx->prog_features, 1);
+	d->occ_p64 = xfg_classify_occupancy(ctx->prog_features, 2);
+	d->occ_p128 = xfg_classify_occupancy(ctx->prog_features, 3);
+	d->occ_s64 = xfg_classify_occupancy(ctx->prog_features, 4);
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -973,6 +990,22 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 		a->streamed = 0;   /* experimental: opt-in until it beats the classic kernel */
 	if (a->streamed)
 		a->window = 64;
+	/* The pipelined kernel takes every fixed-stride batch whose windows can
+	 * be loaded without a length (stride >= window, 16-byte aligned). */
+	a->pipe = !a->streamed && !b->offsets && b->stride >= a->window && !(b->stride & 15) &&
+		  !((uintptr_t)b->data & 15) && b->count < (1ull << 32);
+	if (!ks || strcmp(ks, "pipe"))
+		a->pipe = 0;   /* experimental: opt-in (XFG_KERNEL=pipe) until it beats the classic kernel */
+	/* Speculative single-lookup mode (xfg_spec.hip): IPv4 keys of one
+	 * direction only (census), no live Ethernet or IPv6 lookup. */
+	if (a->pipe && (ctx->prog_features & (1u << 3))) {
+		int v4d = (a->t4.fmask & 2) == 2, v4s = (a->t4.fmask & 1) == 1;
+		int eth_live = a->te.count && (a->te.fmask & 3);
+		int v6_live = a->t6.count && (a->t6.fmask & 3);
+		const char *sp = getenv("XFG_SPEC");   /* diagnostics: "0" disables */
+		a->spec = a->t4.count && v4d != v4s && !eth_live && !v6_live &&
+			  !(sp && !strcmp(sp, "0"));
+	}
 	/* Diagnostics only: XFG_ABLATE=<mask> (1 = treat every table as empty,
 	 * 2 = drop counter atomics, 4 = stage windows only).  Results are wrong
 	 * under any non-zero mask; tools/ablate.py uses it to split time. */
@@ -994,8 +1027,10 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 /* One persistent wave of workgroups: every resident slot of every CU. */
 static unsigned grid_for(const struct xfg_dev *d, const struct xfg_kargs *a)
 {
-	uint64_t tiles = (a->n + 255) / 256;
-	uint64_t per_cu = a->streamed ? d->occ_st : a->window <= 64 ? d->occ64 : d->occ128;
+	uint64_t tiles = (a->n + 255) / 256;   /* pipelined: 4 waves x 64 packets */
+	uint64_t per_cu = a->streamed ? d->occ_st
+			: a->pipe ? (a->window <= 64 ? (a->spec ? d->occ_s64 : d->occ_p64) : d->occ_p128)
+			: a->window <= 64 ? d->occ64 : d->occ128;
 	const char *g = getenv("XFG_GRID_PER_CU");   /* diagnostics only */
 	if (g && *g)
 		per_cu = strtoul(g, NULL, 0);
@@ -1014,6 +1049,78 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	int err = 0;
 	struct xfg_kargs a = *a0;
 	unsigned grid = grid_for(d, &a);
+	if (a.pipe) {
+		/* one list per wave, room for every packet of its tiles */
+		uint64_t nw = (uint64_t)grid * 4, nt = (a.n + 63) / 64;
+		uint64_t cap = (nt + nw - 1) / nw * 64;
+		uint64_t bytes = nw * (cap ? cap : 64) * 4;
+		if (bytes > d->fix_bytes) {
+			hipFree(d->fix);
+			d->fix = NULL;
+			d->fix_bytes = 0;
+			HIPCHK(hipMalloc((void **)&d->fix, bytes));
+			d->fix_bytes = bytes;
+		}
+		a.fix_list = d->fix;
+		a.fix_cap = (uint32_t)cap;
+		/* hit log: room for twice a uniform share of the workgroup's
+		 * packets in each partition (a fuller region spills to atomics) */
+		uint64_t parts = ((uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES + (1u << XFG_HLOG_SHIFT) - 1) >>
+				 XFG_HLOG_SHIFT;
+		const char *cm = getenv("XFG_COUNT");   /* diagnostics: "atomic" */
+		int any = a.t4.count || a.t6.count || a.te.count || a.port_count;
+		if (any && parts <= XFG_HLOG_PARTS_MAX && !(cm && !strcmp(cm, "atomic"))) {
+			uint64_t per_wg = (a.n + grid - 1) / grid;
+			uint64_t hcap = (2 * ((per_wg + parts - 1) / parts) + 32 + 3) & ~3ull;
+			uint64_t lb = parts * grid * hcap * 4, cb = parts * grid * 4;
+			if (lb > d->hlog_bytes) {
+				hipFree(d->hlog);
+				d->hlog = NULL;
+				d->hlog_bytes = 0;
+				HIPCHK(hipMalloc((void **)&d->hlog, lb));
+				d->hlog_bytes = lb;
+			}
+			if (cb > d->hlog_cnt_bytes) {
+				hipFree(d->hlog_cnt);
+				d->hlog_cnt = NULL;
+				d->hlog_cnt_bytes = 0;
+				HIPCHK(hipMalloc((void **)&d->hlog_cnt, cb));
+				d->hlog_cnt_bytes = cb;
+			}
+			a.hlog = d->hlog;
+			a.hlog_cnt = d->hlog_cnt;
+			a.hlog_cap = (uint32_t)hcap;
+			a.hlog_parts = (uint32_t)parts;
+		}
+		/* speculative records: twice a uniform share per (partition,
+		 * workgroup); a fuller region defers its packets to the serial pass */
+		uint64_t sparts = ((uint64_t)a.t4.nbuckets + 1 + (1u << XFG_SLOG_SHIFT) - 1) >> XFG_SLOG_SHIFT;
+		if (a.spec && sparts <= XFG_HLOG_PARTS_MAX) {
+			uint64_t per_wg = (a.n + grid - 1) / grid;
+			uint64_t scap = 2 * ((per_wg + sparts - 1) / sparts) + 16;
+			uint64_t lb = sparts * grid * scap * 16, cb = sparts * grid * 4;
+			if (lb > d->slog_bytes) {
+				hipFree(d->slog);
+				d->slog = NULL;
+				d->slog_bytes = 0;
+				HIPCHK(hipMalloc(&d->slog, lb));
+				d->slog_bytes = lb;
+			}
+			if (cb > d->slog_cnt_bytes) {
+				hipFree(d->slog_cnt);
+				d->slog_cnt = NULL;
+				d->slog_cnt_bytes = 0;
+				HIPCHK(hipMalloc((void **)&d->slog_cnt, cb));
+				d->slog_cnt_bytes = cb;
+			}
+			a.slog = d->slog;
+			a.slog_cnt = d->slog_cnt;
+			a.slog_cap = (uint32_t)scap;
+			a.slog_parts = (uint32_t)sparts;
+		} else {
+			a.spec = 0;
+		}
+	}
 	if (user && user != (void *)d->stream) {
 		HIPCHK(hipEventRecord(d->ev_user, (hipStream_t)user));
 		HIPCHK(hipStreamWaitEvent(d->stream, d->ev_user, 0));

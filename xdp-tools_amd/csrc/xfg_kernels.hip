@@ -60,6 +60,16 @@ constexpr int TILE = 256;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Packet bytes past the staged window, read from HBM through a global-
+// address-space pointer: a generic (flat) load would also count against the
+// LDS counter and complete out of order, so every wait near it degrades to
+// vmcnt(0).
+__device__ __forceinline__ uint32_t gbyte(const uint8_t *p, uint32_t o)
+{
+	return reinterpret_cast<const __attribute__((address_space(1))) uint8_t *>(
+		reinterpret_cast<uintptr_t>(p))[o];
+}
+
 // ---------------------------------------------------------------- packet view
 template <int W>
 struct Pkt {
@@ -73,7 +83,7 @@ struct Pkt {
 	{
 		if (o < (uint32_t)W)
 			return reinterpret_cast<const uint8_t *>(row)[o];
-		return g[o];
+		return gbyte(g, o);
 	}
 	// Little-endian 32-bit load of bytes o..o+3 (o+3 < len).
 	__device__ __forceinline__ uint32_t u32(uint32_t o) const
@@ -82,7 +92,8 @@ struct Pkt {
 			uint32_t lo = row[o >> 2], hi = row[(o >> 2) + 1];
 			return __builtin_amdgcn_alignbyte(hi, lo, o & 3);
 		}
-		return g[o] | (g[o + 1] << 8) | (g[o + 2] << 16) | ((uint32_t)g[o + 3] << 24);
+		return gbyte(g, o) | (gbyte(g, o + 1) << 8) | (gbyte(g, o + 2) << 16) |
+		       (gbyte(g, o + 3) << 24);
 	}
 	// Raw (memory-order) 16-bit value of bytes o, o+1: the BPF u16 load.
 	__device__ __forceinline__ uint32_t raw16(uint32_t o) const
@@ -91,7 +102,7 @@ struct Pkt {
 			uint32_t lo = row[o >> 2], hi = row[(o >> 2) + 1];
 			return __builtin_amdgcn_alignbyte(hi, lo, o & 3) & 0xffffu;
 		}
-		return g[o] | ((uint32_t)g[o + 1] << 8);
+		return gbyte(g, o) | (gbyte(g, o + 1) << 8);
 	}
 	// Network-order 16-bit field as a host value (bpf_ntohs of the load).
 	__device__ __forceinline__ uint32_t be16(uint32_t o) const
@@ -135,6 +146,7 @@ struct Parsed {
 	uint32_t l3;           // 0 none, 1 IPv4, 2 ARP, 3 IPv6
 	uint32_t arp_op;
 	uint32_t k4a, k4b;     // IPv4: dst, src | ARP: sip, tip
+	uint32_t ka_off, kb_off;   // byte offsets of k4a, k4b in the frame
 	uint32_t o6;           // IPv6 header offset (saddr o6+8, daddr o6+24)
 	uint32_t nd;           // NDISC: 0 none, 135 NS, 136 NA
 	uint32_t ond;          // target offset
@@ -165,6 +177,8 @@ __device__ __forceinline__ bool parse_fast(const P &p, Parsed &r)
 			r.l3 = 1;
 			r.k4a = __builtin_amdgcn_alignbyte(d8, d7, 2);   // daddr 30..33
 			r.k4b = __builtin_amdgcn_alignbyte(d7, d6, 2);   // saddr 26..29
+			r.ka_off = 30;
+			r.kb_off = 26;
 			r.psrc = d8 >> 16;                        // bytes 34,35
 			r.pdst = d9 & 0xffff;                     // bytes 36,37
 			if ((FEAT & F_UDP) && proto == 17) {
@@ -213,6 +227,7 @@ __device__ __forceinline__ Parsed parse(const P &p)
 	r.l4proto = 0;
 	r.arp_op = 0;
 	r.k4a = r.k4b = 0;
+	r.ka_off = r.kb_off = 0;
 	r.o6 = r.ond = 0;
 	r.pdst = r.psrc = 0;
 	if (parse_fast<FEAT, W, P>(p, r))
@@ -259,6 +274,8 @@ __device__ __forceinline__ Parsed parse(const P &p)
 			if constexpr ((FEAT & F_IPV4) != 0) {
 				r.k4a = p.u32(off + 16);   // daddr: checked first
 				r.k4b = p.u32(off + 12);   // saddr
+				r.ka_off = off + 16;
+				r.kb_off = off + 12;
 			}
 		} else if ((FEAT & F_IPV4) && proto == 0x0806) {
 			// parse_arphdr (parsing_helpers.h:235-253), xdpfilt_prog.h:241-261
@@ -271,6 +288,8 @@ __device__ __forceinline__ Parsed parse(const P &p)
 			r.arp_op = p.be16(off + 6);
 			r.k4a = p.u32(off + 14);   // sip
 			r.k4b = p.u32(off + 24);   // tip
+			r.ka_off = off + 14;
+			r.kb_off = off + 24;
 			return r;                  // ip_type stays 0: no L4 stage
 		} else if (proto == 0x86DD) {
 			// __parse_ip6hdr + skip_ip6hdrext (parsing_helpers.h:136-199)
@@ -1069,7 +1088,7 @@ struct SPkt {
 	{
 		if (o < 64)
 			return (dw(o >> 2) >> (8 * (o & 3))) & 0xff;
-		return g[o];
+		return gbyte(g, o);
 	}
 	__device__ __forceinline__ uint32_t u32(uint32_t o) const
 	{
@@ -1077,7 +1096,8 @@ struct SPkt {
 			const uint32_t k = o >> 2;
 			return __builtin_amdgcn_alignbyte(dw(k < 15 ? k + 1 : 15), dw(k), o & 3);
 		}
-		return g[o] | (g[o + 1] << 8) | (g[o + 2] << 16) | ((uint32_t)g[o + 3] << 24);
+		return gbyte(g, o) | (gbyte(g, o + 1) << 8) | (gbyte(g, o + 2) << 16) |
+		       (gbyte(g, o + 3) << 24);
 	}
 	__device__ __forceinline__ uint32_t raw16(uint32_t o) const
 	{
@@ -1085,7 +1105,7 @@ struct SPkt {
 			const uint32_t k = o >> 2;
 			return __builtin_amdgcn_alignbyte(dw(k < 15 ? k + 1 : 15), dw(k), o & 3) & 0xffffu;
 		}
-		return g[o] | ((uint32_t)g[o + 1] << 8);
+		return gbyte(g, o) | (gbyte(g, o + 1) << 8);
 	}
 	__device__ __forceinline__ uint32_t be16(uint32_t o) const
 	{
@@ -1124,7 +1144,7 @@ struct RegKeys {
 #pragma unroll
 		for (int i = 0; i < 4; i++) {
 			const uint8_t *q = g + o + 4 * i;
-			k[i] = q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24);
+			k[i] = gbyte(q, 0) | (gbyte(q, 1) << 8) | (gbyte(q, 2) << 16) | (gbyte(q, 3) << 24);
 		}
 	}
 };
@@ -1377,9 +1397,64 @@ __global__ __launch_bounds__(IO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 			atomicAdd(global_counter(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
 }
 
+#include "xfg_pipe.hip"
+#include "xfg_spec.hip"
+
 template <uint32_t FEAT>
 hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 {
+	if constexpr ((FEAT & F_IPV4) != 0) {
+		if (a.pipe && a.spec) {
+			const size_t dl = ((a.hlog ? a.hlog_parts : 0) + a.slog_parts) * 4;
+			if (a.window <= 64) {
+				if (a.dense)
+					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 64, true>), dim3(grid), dim3(TILE), dl, s, a);
+				else
+					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 64, false>), dim3(grid), dim3(TILE), dl, s, a);
+			} else {
+				if (a.dense)
+					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 128, true>), dim3(grid), dim3(TILE), dl, s, a);
+				else
+					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 128, false>), dim3(grid), dim3(TILE), dl, s, a);
+			}
+			hipError_t e = hipGetLastError();
+			if (e != hipSuccess)
+				return e;
+			if (a.hlog) {
+				hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
+				if ((e = hipGetLastError()) != hipSuccess)
+					return e;
+			}
+			if (!(a.ablate & 8))
+				hipLaunchKernelGGL(xfg_spec_resolve_kernel, dim3(a.slog_parts), dim3(SR_THREADS), 0, s, a, grid);
+			return hipGetLastError();
+		}
+	}
+	if (a.pipe) {
+		const size_t dl = a.hlog ? a.hlog_parts * 4 : 0;   // s_pcnt
+		if (a.window <= 64) {
+			if constexpr (FEAT == (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH | F_DENY)) {
+				if (a.dense && a.variant == 0x15) {   // diagnostics: 5 waves/SIMD
+					hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 64, true, 5>), dim3(grid), dim3(TILE), dl, s, a);
+					return hipGetLastError();
+				}
+			}
+			if (a.dense)
+				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 64, true>), dim3(grid), dim3(TILE), dl, s, a);
+			else
+				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 64, false>), dim3(grid), dim3(TILE), dl, s, a);
+		} else {
+			if (a.dense)
+				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 128, true>), dim3(grid), dim3(TILE), dl, s, a);
+			else
+				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 128, false>), dim3(grid), dim3(TILE), dl, s, a);
+		}
+		const hipError_t e = hipGetLastError();
+		if (e != hipSuccess || !a.hlog)
+			return e;
+		hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
+		return hipGetLastError();
+	}
 	if (a.streamed) {
 		hipLaunchKernelGGL((xfg_classify_stream_kernel<FEAT, 0>), dim3(grid), dim3(IO_THREADS), 0, s, a);
 	} else if (a.window <= 64) {
@@ -1458,12 +1533,23 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 
 // Resident workgroups per CU of the classify kernel a launch would use
 // (grid sizing: one persistent wave of workgroups); window 1 = the streamed
-// kernel.
+// kernel, 2 / 3 = the pipelined kernel with a 64 / 128-byte window.
 template <uint32_t FEAT>
 static int occupancy_feat(uint32_t window)
 {
 	int n = 0;
-	hipError_t e = window == 1
+	if constexpr ((FEAT & F_IPV4) != 0) {
+		if (window == 4) {
+			hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+				&n, xfg_classify_spec_kernel<FEAT, 64, true>, TILE, 1024);
+			return e == hipSuccess && n > 0 ? n : 4;
+		}
+	}
+	hipError_t e = window == 2 || window == 4
+		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_pipe_kernel<FEAT, 64, true>, TILE, 0)
+		: window == 3
+		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_pipe_kernel<FEAT, 128, false>, TILE, 0)
+		: window == 1
 		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_stream_kernel<FEAT, 0>, IO_THREADS, 0)
 		: window <= 64
 		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_kernel<FEAT, 64, 0, true>, TILE, 0)

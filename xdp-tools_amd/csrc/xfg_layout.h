@@ -65,6 +65,10 @@
 
 #define XFG_BLOOM_K       4u
 
+#define XFG_HLOG_SHIFT    14u     /* hit-log partition: 16384 counters (64 KiB of LDS) */
+#define XFG_HLOG_PARTS_MAX 4096u  /* partitions a classify workgroup can track */
+#define XFG_SLOG_SHIFT    10u     /* speculative records: 1024 bucket lines per partition */
+
 
 /* Per-hash-map descriptor passed to the kernel by value. */
 struct xfg_tdesc {
@@ -121,6 +125,27 @@ struct xfg_kargs {
 	uint32_t desc_mask;
 	uint32_t desc_first;
 	uint32_t dense;               /* stride == window, no offsets/descriptors */
+	uint32_t pipe;                /* the pipelined kernel (fixed stride >= window) */
+	uint32_t fix_cap;             /* pipelined: deferred-packet list entries per wave */
+	uint32_t *fix_list;           /* pipelined: (grid * 4) lists of fix_cap entries */
+	/* Hit log (pipelined kernel; NULL = memory-side atomics): the counter
+	 * identities of cold hits, partitioned by identity >> XFG_HLOG_SHIFT.
+	 * Workgroup w appends to region (p * grid + w) * hlog_cap of partition p
+	 * and leaves its fill in hlog_cnt[p * grid + w]; xfg_hlog_count_kernel
+	 * sums each partition in LDS into the counters. */
+	uint32_t *hlog;
+	uint32_t *hlog_cnt;
+	uint32_t hlog_cap;
+	uint32_t hlog_parts;
+	/* Speculative single-lookup mode (xfg_spec.hip): 16-byte records per
+	 * (partition of 2^XFG_SLOG_SHIFT home buckets, workgroup), same layout
+	 * as the hit log; spec = 0 when the rule set has more than one live
+	 * lookup per packet. */
+	void *slog;
+	uint32_t *slog_cnt;
+	uint32_t slog_cap;
+	uint32_t slog_parts;
+	uint32_t spec;
 };
 
 
