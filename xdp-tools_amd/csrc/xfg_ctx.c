@@ -1016,6 +1016,7 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	if (ab && *ab) {
 		a->ablate = (uint32_t)strtoul(ab, NULL, 0);
 		if (a->ablate & 1) {
+			a->spec = 0;
 			a->t4.count = a->t6.count = a->te.count = 0;
 			a->port_count = 0;
 		}

@@ -142,42 +142,58 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 		const uint32_t rem = n - base >= 64u ? 64u : n - base;
 		if constexpr (DENSE) {
 			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + lane;
+		// (no zero fill: a register write behind a load still in flight
+		// would wait for it; lanes past the batch end are never parsed)
 #pragma unroll
-			for (int it = 0; it < CPP; it++) {
-				w[it] = u32x4{ 0, 0, 0, 0 };
+			for (int it = 0; it < CPP; it++)
 				if ((uint32_t)(it * 64 + lane) / CPP < rem)
 					w[it] = __builtin_nontemporal_load(src + it * 64);
-			}
 		} else {
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
 				const int c = it * 64 + lane;
 				const uint32_t pk = c / CPP, sub = c % CPP;
-				w[it] = u32x4{ 0, 0, 0, 0 };
 				if (pk < rem)
 					w[it] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
 						a.data + (uint64_t)(base + pk) * a.stride + sub * 16));
 			}
 		}
-		wl = (uint32_t)lane < rem ? load_len(a, base + lane) : 0;
+		if ((uint32_t)lane < rem)
+			wl = load_len(a, base + lane);
 	};
 
-	// windows two tiles ahead: wa = tile i, wb = tile i+1
-	u32x4 wa[CPP], wb[CPP];
-	uint32_t la = 0, lb = 0;
+	// Two window buffers and two S1 -> S2 state sets alternate roles: tile
+	// i's windows live in buffer i % 2 and are refilled with tile i+2 once
+	// staged; S1 of tile i fills state i % 2, S2 of tile i-1 reads the other.
+	// The loop is unrolled by two so no register holding a load in flight is
+	// ever copied (a copy would wait for the load, serialising the pipeline).
+	struct Win {
+		u32x4 w[CPP];
+		uint32_t len;
+	};
+	// inf: bit 0 valid, 1-3 abort stage, 4 has the lookup, 5 zero key
+	struct S12 {
+		uint32_t inf, pt, len, key, h;
+		unsigned long long bw;
+	};
+	Win W0, W1;
+	W0.len = W1.len = 0;
+	S12 X0 = { 0, CT_NONE, 0, 0, 0, 0 }, X1 = { 0, CT_NONE, 0, 0, 0, 0 };
 	if (my_nt)
-		load_win(tile_of(0), wa, la);
+		load_win(tile_of(0), W0.w, W0.len);
 	if (my_nt > 1)
-		load_win(tile_of(1), wb, lb);
-	// S1 -> S2: inf bit 0 valid, 1-3 abort stage, 4 has the lookup, 5 zero key
-	uint32_t inf1 = 0, pt1 = CT_NONE, len1 = 0, key1 = 0, h1 = 0;
-	unsigned long long bw1 = 0;
+		load_win(tile_of(1), W1.w, W1.len);
 
-	for (uint32_t i = 0; i < my_nt + 1; i++) {
+	auto body = [&](uint32_t i, Win &Wc, const S12 &Sp, S12 &Sn) {
 		const bool s1 = i < my_nt, s2 = i >= 1;
 		// ------------------------------------------------ S1 (tile i)
-		uint32_t inf1n = 0, pt1n = CT_NONE, len1n = 0, key1n = 0, h1n = 0;
-		unsigned long long bw1n = 0;
+		// (Sn.bw is not cleared: it is read only where inf bit 4 says the
+		// load was issued, and a clear would wait for the old load)
+		Sn.inf = 0;
+		Sn.pt = CT_NONE;
+		Sn.len = 0;
+		Sn.key = 0;
+		Sn.h = 0;
 		bool df = false;
 		const uint32_t gi1 = tile_of(i) * 64 + lane;
 		if (s1) {
@@ -187,15 +203,15 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 				const int c = it * 64 + lane;
 				const int pk = c / CPP, sub = c % CPP;
 				uint32_t *d = &wrows[pk * ROWDW + sub * 4];
-				d[0] = wa[it].x;
-				d[1] = wa[it].y;
-				d[2] = wa[it].z;
-				d[3] = wa[it].w;
+				d[0] = Wc.w[it].x;
+				d[1] = Wc.w[it].y;
+				d[2] = Wc.w[it].z;
+				d[3] = Wc.w[it].w;
 			}
-			len1n = la;
+			Sn.len = Wc.len;
 			__builtin_amdgcn_wave_barrier();
 			if (gi1 < n) {
-				Pkt<W> p{ myrow, nullptr, len1n };
+				Pkt<W> p{ myrow, nullptr, Sn.len };
 				Parsed r;
 				r.abort_at = NST;
 				r.l3 = 0;
@@ -203,64 +219,60 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 				const bool fast = parse_fast<FEAT, W>(p, r);
 				df = !fast;
 				if (fast) {
-					inf1n = 1 | (r.abort_at << 1);
+					Sn.inf = 1 | (r.abort_at << 1);
 					if constexpr (PORTS) {
 						if (r.abort_at == NST && a.port_count && r.l4proto) {
 							const uint32_t pm = r.l4proto == 17 ? M_UDP : M_TCP;
 							uint32_t t = CT_NONE;
 							if (check_port(a, s_pbits, r.pdst, M_DST | pm, t) ||
 							    check_port(a, s_pbits, r.psrc, M_SRC | pm, t))
-								pt1n = t;
+								Sn.pt = t;
 						}
 					}
 					if (r.l3 == 1) {
-						key1n = row32(myrow, koff);
-						if (key1n == 0) {
-							inf1n |= 16 | 32;
+						Sn.key = row32(myrow, koff);
+						if (Sn.key == 0) {
+							Sn.inf |= 16 | 32;
 						} else {
-							inf1n |= 16;
-							h1n = xfg_hash_v4(key1n, a.t4.seed);
+							Sn.inf |= 16;
+							Sn.h = xfg_hash_v4(Sn.key, a.t4.seed);
 							if (a.t4.bloom_words)
-								bw1n = a.t4.bloom[xfg_bloom_word(h1n, a.t4.bloom_words)];
+								Sn.bw = a.t4.bloom[xfg_bloom_word(Sn.h, a.t4.bloom_words)];
 						}
 					}
 				}
 			}
 		}
 		// ------------------------------------------------ windows of tile i+2
-#pragma unroll
-		for (int it = 0; it < CPP; it++)
-			wa[it] = wb[it];
-		la = lb;
 		if (i + 2 < my_nt)
-			load_win(tile_of(i + 2), wb, lb);
+			load_win(tile_of(i + 2), Wc.w, Wc.len);
 		// ------------------------------------------------ S2 (tile i-1)
 		uint32_t act = A_NONE, tag = CT_NONE;
 		bool fk = false;
 		const uint32_t gi2 = s2 ? tile_of(i - 1) * 64 + lane : 0;
-		if (s2 && (inf1 & 1)) {
-			const uint32_t ab = (inf1 >> 1) & 7;
-			const uint32_t alt_act = ab != NST ? A_ABORTED : pt1 != CT_NONE ? HIT : MISS;
-			const uint32_t alt_tag = ab != NST ? CT_NONE : pt1;
+		if (s2 && (Sp.inf & 1)) {
+			const uint32_t ab = (Sp.inf >> 1) & 7;
+			const uint32_t alt_act = ab != NST ? A_ABORTED : Sp.pt != CT_NONE ? HIT : MISS;
+			const uint32_t alt_tag = ab != NST ? CT_NONE : Sp.pt;
 			bool maybe = false;
-			if (inf1 & 16) {
-				if (inf1 & 32) {
+			if (Sp.inf & 16) {
+				if (Sp.inf & 32) {
 					maybe = a.t4.zero_present;
 				} else {
-					const unsigned long long bm = xfg_bloom_mask(h1);
-					maybe = !a.t4.bloom_words || (bw1 & bm) == bm;
+					const unsigned long long bm = xfg_bloom_mask(Sp.h);
+					maybe = !a.t4.bloom_words || (Sp.bw & bm) == bm;
 				}
 			}
 			if (maybe) {
 				act = HIT;
 				if (!(a.ablate & 8)) {
-					const uint32_t b = (inf1 & 32) ? a.t4.nbuckets : xfg_home(h1, a.t4.nbuckets);
+					const uint32_t b = (Sp.inf & 32) ? a.t4.nbuckets : xfg_home(Sp.h, a.t4.nbuckets);
 					const uint32_t p = b >> XFG_SLOG_SHIFT;
 					const uint32_t pos = atomicAdd(&s_scnt[p], 1u);
 					if (pos < a.slog_cap) {
-						const u32x4 rec = { gi2, key1, alt_tag,
+						const u32x4 rec = { gi2, Sp.key, alt_tag,
 								    alt_act | (kmask << 4) | (HIT << 8) |
-								    ((inf1 & 32) ? 1u << 12 : 0u) };
+								    ((Sp.inf & 32) ? 1u << 12 : 0u) };
 						static_cast<u32x4 *>(a.slog)[((uint64_t)p * gridDim.x +
 									      blockIdx.x) * a.slog_cap + pos] = rec;
 					} else {
@@ -283,14 +295,13 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 			if (a.ablate & 2)
 				tag = CT_NONE;
 			bump(tag);
-			count_stats(act, len1);
+			count_stats(act, Sp.len);
 		}
-		inf1 = inf1n;
-		pt1 = pt1n;
-		len1 = len1n;
-		key1 = key1n;
-		h1 = h1n;
-		bw1 = bw1n;
+	};
+	for (uint32_t i = 0; i < my_nt + 1; i += 2) {
+		body(i, W0, X1, X0);
+		if (i + 1 < my_nt + 1)
+			body(i + 1, W1, X0, X1);
 	}
 	// ---- the deferred packets, serially
 	if (nfix) {
@@ -346,6 +357,10 @@ __global__ __launch_bounds__(SR_THREADS) void xfg_spec_resolve_kernel(const xfg_
 {
 	__shared__ u32x4 lines[SLOG_LB * 4];
 	__shared__ uint32_t cnt[SLOG_LB * XFG_SLOTS_V4];
+	// false positives: stats deltas and the counters they fall through to
+	// (a ruled port is hot) are summed here, not with contended atomics
+	__shared__ unsigned long long s_fix[6];
+	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
 	const uint32_t p = blockIdx.x, tid = threadIdx.x;
 	const uint32_t b0 = p * SLOG_LB;
 	const uint32_t nb = a.t4.nbuckets + 1 - b0 < SLOG_LB ? a.t4.nbuckets + 1 - b0 : SLOG_LB;
@@ -354,13 +369,28 @@ __global__ __launch_bounds__(SR_THREADS) void xfg_spec_resolve_kernel(const xfg_
 		lines[i] = src[i];
 	for (uint32_t i = tid; i < SLOG_LB * XFG_SLOTS_V4; i += SR_THREADS)
 		cnt[i] = 0;
+	if (tid < 6)
+		s_fix[tid] = 0;
+	for (uint32_t i = tid; i < CC_ENTRIES; i += SR_THREADS) {
+		s_ctag[i] = CT_NONE;
+		s_ccnt[i] = 0;
+	}
 	__syncthreads();
 	for (uint32_t w = tid; w < grid; w += SR_THREADS) {
 		const uint64_t r = (uint64_t)p * grid + w;
 		const uint32_t c = a.slog_cnt[r];
 		const u32x4 *e = static_cast<const u32x4 *>(a.slog) + r * a.slog_cap;
-		for (uint32_t k = 0; k < c; k++) {
-			const u32x4 rec = e[k];
+		for (uint32_t k0 = 0; k0 < c; k0 += 4) {
+		// four records in flight per thread (they are independent)
+		u32x4 rq[4];
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+			rq[q] = k0 + q < c ? __builtin_nontemporal_load(e + k0 + q) : u32x4{ 0, 0, 0, 0 };
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			if (k0 + q >= c)
+				break;
+			const u32x4 rec = rq[q];
 			const uint32_t gi = rec.x, key = rec.y, alt_tag = rec.z, meta = rec.w;
 			const uint32_t mask = (meta >> 4) & 15, hit_act = (meta >> 8) & 3,
 				       alt_act = meta & 15;
@@ -395,18 +425,24 @@ __global__ __launch_bounds__(SR_THREADS) void xfg_spec_resolve_kernel(const xfg_
 				// Bloom false positive: the packet continues past the
 				// lookup, as the reference program does
 				a.verdicts[gi] = (uint8_t)alt_act;
-				if (alt_tag != CT_NONE)
+				if (alt_tag != CT_NONE && !cache_hit(s_ctag, s_ccnt, alt_tag, 1))
 					atomicAdd(global_counter(a, alt_tag), 1ull);
 				const unsigned long long len = load_len(a, gi);
-				atomicAdd(&a.stats[hit_act * 2], ~0ull);          // -1
-				atomicAdd(&a.stats[hit_act * 2 + 1], 0ull - len);
-				atomicAdd(&a.stats[alt_act * 2], 1ull);
-				atomicAdd(&a.stats[alt_act * 2 + 1], len);
+				atomicAdd(&s_fix[hit_act * 2], ~0ull);          // -1
+				atomicAdd(&s_fix[hit_act * 2 + 1], 0ull - len);
+				atomicAdd(&s_fix[alt_act * 2], 1ull);
+				atomicAdd(&s_fix[alt_act * 2 + 1], len);
 			}
+		}
 		}
 	}
 	__syncthreads();
 	for (uint32_t i = tid; i < nb * XFG_SLOTS_V4; i += SR_THREADS)
 		if (cnt[i])
 			atomicAdd(a.t4.hits + (uint64_t)b0 * XFG_SLOTS_V4 + i, (unsigned long long)cnt[i]);
+	if (tid < 6 && s_fix[tid])
+		atomicAdd(&a.stats[tid], s_fix[tid]);
+	for (uint32_t i = tid; i < CC_ENTRIES; i += SR_THREADS)
+		if (s_ctag[i] != CT_NONE && s_ccnt[i])
+			atomicAdd(global_counter(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
 }
