@@ -130,6 +130,22 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0:
         cpu = cpu_baseline(X, np, v4, ports, args.cpu_seconds)
 
+    # ---- traffic: fabric bytes per launch of the same kernel on the same
+    # workload, from the committed rocprofv3 --pmc passes (a PMC pass cannot
+    # run inside this timed process); null for any other configuration
+    traffic, traffic_src = None, None
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                       "r01_v6_pmc_classic_mask0.json")
+    default_cfg = (args.rules == 1_000_000 and args.log2_packets == 24 and
+                   not any(k.startswith("XFG_") for k in os.environ))
+    if default_cfg and os.path.exists(pmc):
+        with open(pmc) as fh:
+            pm = json.load(fh)
+        traffic = int(pm["fetch_bytes_x2"] + pm["write_bytes"])
+        traffic_src = ("profiles/r01_v6_pmc_classic_mask0.json: rocprofv3 --pmc FETCH_SIZE x2 "
+                       "(gfx950 half-count correction) + WRITE_SIZE per launch; L2 memory-side "
+                       "bytes, Infinity-Cache hits included")
+
     total_pkts = n * args.steps * world
     value = total_pkts / wall / 1e6
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
@@ -161,11 +177,12 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
             "alg_bytes_per_launch": alg_bytes,
             "kernel_ms": round(kern_ms, 4),
             "peak_measured_stream_read": round(peak_meas, 1),
             "frac_of_measured": round(achieved / peak_meas, 4),
+            "traffic_source": traffic_src,
         },
         "cpu_baseline": cpu,
         "gen_seconds": round(gen_s, 2),
