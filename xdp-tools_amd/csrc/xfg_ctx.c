@@ -1064,12 +1064,17 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		}
 		a.fix_list = d->fix;
 		a.fix_cap = (uint32_t)cap;
-		/* hit log: room for twice a uniform share of the workgroup's
-		 * packets in each partition (a fuller region spills to atomics) */
-		uint64_t parts = ((uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES + (1u << XFG_HLOG_SHIFT) - 1) >>
-				 XFG_HLOG_SHIFT;
-		const char *cm = getenv("XFG_COUNT");   /* diagnostics: "atomic" */
-		int any = a.t4.count || a.t6.count || a.te.count || a.port_count;
+	}
+	/* hit log (pipelined kernels, and the classic kernel's production build):
+	 * room for twice a uniform share of the workgroup's packets in each
+	 * partition (a fuller region spills to atomics) */
+	uint64_t parts = ((uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES + (1u << XFG_HLOG_SHIFT) - 1) >>
+			 XFG_HLOG_SHIFT;
+	const char *cm = getenv("XFG_COUNT");   /* diagnostics: "atomic" | "log" */
+	int any = a.t4.count || a.t6.count || a.te.count || a.port_count;
+	/* (measured on C3: the classic kernel is faster with atomics, 0.467 ms
+	 * against 0.51 with the log, so there the log is opt-in) */
+	if (!a.streamed && (a.pipe || (!a.variant && cm && !strcmp(cm, "log")))) {
 		if (any && parts <= XFG_HLOG_PARTS_MAX && !(cm && !strcmp(cm, "atomic"))) {
 			uint64_t per_wg = (a.n + grid - 1) / grid;
 			uint64_t hcap = (2 * ((per_wg + parts - 1) / parts) + 32 + 3) & ~3ull;

@@ -560,6 +560,22 @@ __device__ __forceinline__ unsigned long long *global_counter(const xfg_kargs &a
 	return a.t4.hits + g;
 }
 
+// One cold counter bump: appended to the workgroup's region of its hit-log
+// partition (a plain store; xfg_hlog_count_kernel adds the regions up), or,
+// with no log or a full region, a memory-side atomic.
+__device__ __forceinline__ void cold_bump(const xfg_kargs &a, uint32_t *s_pcnt, uint32_t tag)
+{
+	if (a.hlog) {
+		const uint32_t p = tag >> XFG_HLOG_SHIFT;
+		const uint32_t pos = atomicAdd(&s_pcnt[p], 1u);
+		if (pos < a.hlog_cap) {
+			a.hlog[((uint64_t)p * gridDim.x + blockIdx.x) * a.hlog_cap + pos] = tag;
+			return;
+		}
+	}
+	atomicAdd(global_counter(a, tag), 1ull);
+}
+
 // CHECK_MAP (xdp-filter/xdpfilt_prog.h:56-64): hit iff the key exists and
 // (value & mask) == mask; the counter bump is deferred to the caller.
 __device__ __forceinline__ bool take(const Hit &h, uint32_t mask, uint32_t base, uint32_t &tag)
@@ -794,6 +810,7 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 	__shared__ uint32_t s_pbits[PORTS ? 2048 : 1];
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
 	__shared__ unsigned long long s_stats[6];
+	extern __shared__ uint32_t s_pcnt[];   // hit-log fill per partition (hlog_parts)
 
 	const int tid = threadIdx.x;
 	const int lane = tid & 63;
@@ -803,6 +820,9 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 		s_ctag[i] = CT_NONE;
 		s_ccnt[i] = 0;
 	}
+	if (a.hlog)
+		for (uint32_t i = tid; i < a.hlog_parts; i += TILE)
+			s_pcnt[i] = 0;
 	if constexpr (PORTS) {
 		if (a.port_count)
 			for (int i = tid; i < 2048; i += TILE)
@@ -950,15 +970,19 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 				const unsigned long long same = __ballot(mine);
 				if (lane == leader) {
 					const uint32_t cnt = (uint32_t)__popcll(same);
-					if (!cache_hit(s_ctag, s_ccnt, lt, cnt))
-						atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
+					if (!cache_hit(s_ctag, s_ccnt, lt, cnt)) {
+						if (cnt > 1)
+							atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
+						else
+							cold_bump(a, s_pcnt, lt);
+					}
 				}
 				if (mine)
 					tag = CT_NONE;
 			}
 		}
 		if (tag != CT_NONE && !cache_hit(s_ctag, s_ccnt, tag, 1))
-			atomicAdd(global_counter(a, tag), 1ull);
+			cold_bump(a, s_pcnt, tag);
 
 		// 5. per-action stats (xdp_stats_record_action), kept per lane
 #ifdef XFG_EXP_NO_STATS
@@ -1002,6 +1026,10 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 	for (int i = tid; i < CC_ENTRIES; i += TILE)
 		if (s_ctag[i] != CT_NONE && s_ccnt[i])
 			atomicAdd(global_counter(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
+	if (a.hlog)
+		for (uint32_t p = tid; p < a.hlog_parts; p += TILE)
+			a.hlog_cnt[(uint64_t)p * gridDim.x + blockIdx.x] =
+				s_pcnt[p] < a.hlog_cap ? s_pcnt[p] : a.hlog_cap;
 }
 
 // ---------------------------------------------------------------- streamed kernel
@@ -1455,8 +1483,10 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 		hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
 		return hipGetLastError();
 	}
+	const size_t dl = a.hlog ? a.hlog_parts * 4 : 0;   // classic kernel's s_pcnt
 	if (a.streamed) {
 		hipLaunchKernelGGL((xfg_classify_stream_kernel<FEAT, 0>), dim3(grid), dim3(IO_THREADS), 0, s, a);
+		return hipGetLastError();
 	} else if (a.window <= 64) {
 		// build variants of the headline program (diagnostics: XFG_VARIANT)
 		if constexpr (FEAT == (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH | F_DENY)) {
@@ -1494,12 +1524,16 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 			}
 		}
 		if (a.dense)
-			hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 0, true>), dim3(grid), dim3(TILE), 0, s, a);
+			hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 0, true>), dim3(grid), dim3(TILE), dl, s, a);
 		else
-			hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 0>), dim3(grid), dim3(TILE), 0, s, a);
+			hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 0>), dim3(grid), dim3(TILE), dl, s, a);
 	} else {
-		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128, 0>), dim3(grid), dim3(TILE), 0, s, a);
+		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128, 0>), dim3(grid), dim3(TILE), dl, s, a);
 	}
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess || !a.hlog)
+		return e;
+	hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
 	return hipGetLastError();
 }
 
