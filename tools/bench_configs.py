@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""tools/bench_configs.py — the BASELINE.json configurations beside C3
+(SURVEY.md §8d), one GPU, one JSON line each:
+
+  c2  xdpfilt_dny_ip, 1k IPv4 dst rules, 64 B frames, device-resident
+  c4  xdpfilt_dny_all, IMIX 64/570/1514 (7:4:1), 1M IPv4 rules: one GPU's
+      shard of the 8-GPU configuration (weak scaling: per-GPU work fixed)
+  c5  xdpfilt_dny_all, 1514 B frames, 15M IPv4 + 1M IPv6 dst rules + 1024
+      dst-port rules: device-resident, and end to end from host memory
+      (whole frames H2D, verdicts D2H, xfg_classify_host)
+
+Roofline bytes per packet are min(len, 128) + 1.
+Usage: python3 tools/bench_configs.py [c2] [c4] [c5] [--log2-packets N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "xdp-tools_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0
+
+
+def run(name, args):
+    import numpy as np
+    import xftools as X
+    import xfgpu as G
+    kind = {"c2": 2, "c4": 4, "c5": 5}[name]
+    n = 1 << (args.log2_packets or {"c2": 24, "c4": 21, "c5": 20}[name])
+    stride = 64 if kind == 2 else 1536
+    n4 = {2: 1000, 4: 1_000_000, 5: 15_000_000}[kind]
+    n6 = 1_000_000 if kind == 5 else 0
+    nports = 1024 if kind == 5 else 16
+    t0 = time.time()
+    v4 = X.rand_keys(kind, int(n4 * 1.02) + 16, 4)[:n4]
+    v6 = X.rand_keys(kind + 100, int(n6 * 1.02) + 16, 16)[:n6] if n6 else None
+    ports = (np.arange(nports, dtype=np.uint32) * 61 + 53).astype(np.uint16)
+    print(f"[{name}] keys {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    data, lens = X.gen_workload(kind, kind, n, stride, v4=v4, v6=v6, ports=ports)
+    print(f"[{name}] frames {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    feats = G.FEAT_IPV4 | G.FEAT_IPV6 | G.FEAT_DENY if kind == 2 else G.FEAT_ALL | G.FEAT_DENY
+    f = G.Filter(feats, devices=[0], ipv4_capacity=n4, ipv6_capacity=max(n6, 1024))
+    f.update_batch(G.MAP_IPV4, v4, np.full(len(v4), 2, np.uint64))
+    if n6:
+        f.update_batch(G.MAP_IPV6, v6, np.full(len(v6), 2, np.uint64))
+    if kind != 2:
+        pk = np.array([X.port_key(int(p)) for p in ports], "<u4").view(np.uint8)
+        f.update_batch(G.MAP_PORTS, pk, np.full(len(ports), 2 | 4 | 8, np.uint64))
+    setup_s = time.time() - t0
+    print(f"[{name}] rules loaded {setup_s:.1f}s", file=sys.stderr, flush=True)
+    alg = int(np.minimum(lens.astype(np.int64), 128).sum() + n)
+    d_data, d_lens, d_verd = f.alloc(data.nbytes), f.alloc(lens.nbytes), f.alloc(n)
+    d_data.upload(data)
+    d_lens.upload(lens)
+    f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, 2)
+    ms = f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, args.iters)
+    line = {"config": name, "program": f.prog_name, "packets": n, "stride": stride,
+            "rules_ipv4": n4, "rules_ipv6": n6, "port_rules": nports if kind != 2 else 0,
+            "kernel_ms": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+            "roofline": {"alg_bytes_per_launch": alg,
+                         "achieved_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "setup_s": round(setup_s, 1)}
+    if kind == 5:
+        # end to end from host memory: whole frames and lengths H2D, verdicts D2H
+        f.classify_host(data, lens, stride=stride)
+        t1 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            f.classify_host(data, lens, stride=stride)
+        hs = (time.perf_counter() - t1) / reps
+        line["host_path"] = {"Mpps": round(n / hs / 1e6, 2), "ms": round(hs * 1e3, 2),
+                             "GBps_h2d": round(data.nbytes / hs / 1e9, 1),
+                             "note": "whole 1514 B frames at a 1536 B stride H2D + u32 lens, "
+                                     "verdicts D2H, double-buffered pinned staging"}
+    f.close()
+    print(json.dumps(line), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c2", "c4", "c5"])
+    ap.add_argument("--log2-packets", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    for c in a.configs:
+        run(c, a)
+
+
+if __name__ == "__main__":
+    main()
