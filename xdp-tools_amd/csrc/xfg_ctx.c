@@ -73,6 +73,12 @@ struct xfg_dev {
 	void *slog;                     /* speculative records */
 	uint32_t *slog_cnt;
 	uint64_t slog_bytes, slog_cnt_bytes;
+	/* host-resident classify: persistent double-buffered staging */
+	uint8_t *hs_hbuf[2], *hs_dbuf[2], *hs_dv[2];
+	uint32_t *hs_hl[2], *hs_dl[2];
+	hipStream_t hs_st[2];
+	hipEvent_t hs_done[2];
+	size_t hs_bytes;
 	uint32_t *fix;                  /* pipelined kernel: deferred-packet lists */
 	uint64_t fix_bytes;
 	uint32_t *hlog, *hlog_cnt;      /* pipelined kernel: hit log */
@@ -199,6 +205,19 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->port_tab);
 	free(d->port_flags_h);
 	hipFree(d->cstatus);
+	for (int k = 0; k < 2; k++) {
+		if (d->hs_st[k])
+			hipStreamSynchronize(d->hs_st[k]);
+		hipHostFree(d->hs_hbuf[k]);
+		hipHostFree(d->hs_hl[k]);
+		hipFree(d->hs_dbuf[k]);
+		hipFree(d->hs_dl[k]);
+		hipFree(d->hs_dv[k]);
+		if (d->hs_done[k])
+			hipEventDestroy(d->hs_done[k]);
+		if (d->hs_st[k])
+			hipStreamDestroy(d->hs_st[k]);
+	}
 	hipFree(d->fix);
 	hipFree(d->hlog);
 	hipFree(d->hlog_cnt);
@@ -1306,7 +1325,98 @@ fail:
  * pipelined over two streams.  Whole frames cross PCIe (re-packed at a fixed
  * 16-byte-aligned stride): a verdict may depend on bytes past any fixed
  * header window (long IPv6 extension chains, TCP doff bounds checks against
- * the full length), see DESIGN.md "host-resident rate". */
+ * the full length), see DESIGN.md "host-resident rate".  The staging buffers
+ * and streams persist in the device (grown on demand), and the repack into
+ * pinned memory is split over threads (one memcpy per chunk slice when the
+ * batch already has a fixed stride). */
+#define HOST_CH (1u << 18)   /* packets per chunk */
+#define HOST_THREADS 8
+
+struct repack_job {
+	const struct xfg_batch *b;
+	uint8_t *dst;
+	uint32_t *dl;
+	uint64_t first, m;       /* packets [first, first + m) of the batch */
+	uint32_t stride;         /* staging stride */
+	int contiguous;          /* batch stride == staging stride, no offsets */
+};
+
+static void *repack_run(void *arg)
+{
+	struct repack_job *j = arg;
+	const struct xfg_batch *b = j->b;
+	if (j->contiguous) {
+		memcpy(j->dst, (const uint8_t *)b->data + j->first * (uint64_t)j->stride,
+		       j->m * (uint64_t)j->stride);
+	}
+	for (uint64_t i = 0; i < j->m; i++) {
+		uint64_t gi = j->first + i;
+		uint32_t l = b->lens_u16 ? ((const uint16_t *)b->lens)[gi]
+					 : ((const uint32_t *)b->lens)[gi];
+		if (!j->contiguous) {
+			const uint8_t *src = (const uint8_t *)b->data +
+					     (b->offsets ? b->offsets[gi] : gi * (uint64_t)b->stride);
+			memcpy(j->dst + i * (uint64_t)j->stride, src, l);
+		}
+		j->dl[i] = l;
+	}
+	return NULL;
+}
+
+/* m packets from `first` into staging: HOST_THREADS slices in parallel */
+static void repack(const struct xfg_batch *b, uint8_t *dst, uint32_t *dl, uint64_t first,
+		   uint64_t m, uint32_t stride, int contiguous)
+{
+	struct repack_job jobs[HOST_THREADS];
+	pthread_t th[HOST_THREADS];
+	int started[HOST_THREADS] = { 0 };
+	uint64_t per = (m + HOST_THREADS - 1) / HOST_THREADS;
+	for (int t = 0; t < HOST_THREADS; t++) {
+		uint64_t s0 = t * per, s1 = s0 + per < m ? s0 + per : m;
+		jobs[t] = (struct repack_job){ b, dst + s0 * (uint64_t)stride, dl + s0, first + s0,
+					       s1 > s0 ? s1 - s0 : 0, stride, contiguous };
+		if (t && jobs[t].m && m >= 4096)
+			started[t] = !pthread_create(&th[t], NULL, repack_run, &jobs[t]);
+	}
+	for (int t = HOST_THREADS - 1; t >= 0; t--) {   /* the ones not handed off, here */
+		if (!started[t] && jobs[t].m && (t == 0 || m < 4096 || !started[t]))
+			repack_run(&jobs[t]);
+	}
+	for (int t = 1; t < HOST_THREADS; t++)
+		if (started[t])
+			pthread_join(th[t], NULL);
+}
+
+static int host_staging(struct xfg_dev *d, size_t chunk_bytes)
+{
+	int err = 0;
+	if (!d->hs_st[0]) {
+		for (int k = 0; k < 2; k++) {
+			HIPCHK(hipStreamCreateWithFlags(&d->hs_st[k], hipStreamNonBlocking));
+			HIPCHK(hipEventCreate(&d->hs_done[k]));
+			HIPCHK(hipHostMalloc((void **)&d->hs_hl[k], HOST_CH * 4, hipHostMallocDefault));
+			HIPCHK(hipMalloc((void **)&d->hs_dl[k], HOST_CH * 4));
+			HIPCHK(hipMalloc((void **)&d->hs_dv[k], HOST_CH));
+		}
+	}
+	if (chunk_bytes > d->hs_bytes) {
+		for (int k = 0; k < 2; k++) {
+			hipHostFree(d->hs_hbuf[k]);
+			hipFree(d->hs_dbuf[k]);
+			d->hs_hbuf[k] = NULL;
+			d->hs_dbuf[k] = NULL;
+		}
+		d->hs_bytes = 0;
+		for (int k = 0; k < 2; k++) {
+			HIPCHK(hipHostMalloc((void **)&d->hs_hbuf[k], chunk_bytes, hipHostMallocDefault));
+			HIPCHK(hipMalloc((void **)&d->hs_dbuf[k], chunk_bytes));
+		}
+		d->hs_bytes = chunk_bytes;
+	}
+fail:
+	return err;
+}
+
 int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verdicts)
 {
 	int err = 0;
@@ -1319,7 +1429,6 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t 
 	if (!b->count)
 		return 0;
 	struct xfg_dev *d = &ctx->dev[dev];
-	const uint64_t CH = 1u << 18;   /* packets per chunk */
 	uint64_t maxlen = 0;
 	for (uint64_t i = 0; i < b->count; i++) {
 		uint64_t l = b->lens_u16 ? ((const uint16_t *)b->lens)[i] : ((const uint32_t *)b->lens)[i];
@@ -1329,63 +1438,40 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t 
 	uint32_t stride = (uint32_t)((maxlen + 15) & ~15ull);
 	if (stride < 64)
 		stride = 64;
-	size_t chunk_bytes = (size_t)CH * stride;
-	uint8_t *hbuf[2] = { NULL, NULL }, *dbuf[2] = { NULL, NULL }, *dv[2] = { NULL, NULL };
-	uint32_t *hl[2] = { NULL, NULL }, *dl[2] = { NULL, NULL };
-	hipStream_t st[2] = { NULL, NULL };
-	hipEvent_t done[2] = { NULL, NULL };
+	/* a fixed-stride batch whose stride fits is staged as it lies */
+	int contiguous = !b->offsets && b->stride >= stride && !(b->stride & 15);
+	if (contiguous)
+		stride = b->stride;
+	size_t chunk_bytes = (size_t)HOST_CH * stride;
 
 	HIPCHK(hipSetDevice(d->ordinal));
-	for (int k = 0; k < 2; k++) {
-		HIPCHK(hipHostMalloc((void **)&hbuf[k], chunk_bytes, hipHostMallocDefault));
-		HIPCHK(hipHostMalloc((void **)&hl[k], CH * 4, hipHostMallocDefault));
-		HIPCHK(hipMalloc((void **)&dbuf[k], chunk_bytes));
-		HIPCHK(hipMalloc((void **)&dl[k], CH * 4));
-		HIPCHK(hipMalloc((void **)&dv[k], CH));
-		HIPCHK(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
-		HIPCHK(hipEventCreate(&done[k]));
-	}
-	for (uint64_t c = 0, k = 0; c < b->count; c += CH, k ^= 1) {
-		uint64_t m = b->count - c < CH ? b->count - c : CH;
-		HIPCHK(hipEventSynchronize(done[k]));   /* staging buffer k free again */
-		for (uint64_t i = 0; i < m; i++) {
-			uint64_t gi = c + i;
-			uint32_t l = b->lens_u16 ? ((const uint16_t *)b->lens)[gi] : ((const uint32_t *)b->lens)[gi];
-			const uint8_t *src = (const uint8_t *)b->data +
-					     (b->offsets ? b->offsets[gi] : gi * (uint64_t)b->stride);
-			memcpy(hbuf[k] + i * stride, src, l);
-			hl[k][i] = l;
-		}
-		HIPCHK(hipMemcpyAsync(dbuf[k], hbuf[k], m * stride, hipMemcpyHostToDevice, st[k]));
-		HIPCHK(hipMemcpyAsync(dl[k], hl[k], m * 4, hipMemcpyHostToDevice, st[k]));
-		struct xfg_batch sub = { dbuf[k], NULL, dl[k], m, stride, 0 };
+	if ((err = host_staging(d, chunk_bytes)))
+		goto fail;
+	for (uint64_t c = 0, k = 0; c < b->count; c += HOST_CH, k ^= 1) {
+		uint64_t m = b->count - c < HOST_CH ? b->count - c : HOST_CH;
+		HIPCHK(hipEventSynchronize(d->hs_done[k]));   /* staging buffer k free again */
+		repack(b, d->hs_hbuf[k], d->hs_hl[k], c, m, stride, contiguous);
+		HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], d->hs_hbuf[k], m * stride, hipMemcpyHostToDevice,
+				      d->hs_st[k]));
+		HIPCHK(hipMemcpyAsync(d->hs_dl[k], d->hs_hl[k], m * 4, hipMemcpyHostToDevice, d->hs_st[k]));
+		struct xfg_batch sub = { d->hs_dbuf[k], NULL, d->hs_dl[k], m, stride, 0 };
 		struct xfg_kargs a;
 		pthread_mutex_lock(&ctx->lock);
 		ctx->reduced = 0;
-		err = fill_kargs(ctx, d, &sub, dv[k], &a);
+		err = fill_kargs(ctx, d, &sub, d->hs_dv[k], &a);
 		pthread_mutex_unlock(&ctx->lock);
 		if (err)
 			goto fail;
-		/* copies on st[k]; the kernels on the device stream (launch_batch
-		 * orders it after st[k]'s uploads and st[k] after the kernels) */
-		if ((err = launch_batch(ctx, d, &a, st[k], 1)))
+		/* copies on hs_st[k]; the kernels on the device stream (launch_batch
+		 * orders it after hs_st[k]'s uploads and hs_st[k] after the kernels) */
+		if ((err = launch_batch(ctx, d, &a, d->hs_st[k], 1)))
 			goto fail;
-		HIPCHK(hipMemcpyAsync(verdicts + c, dv[k], m, hipMemcpyDeviceToHost, st[k]));
-		HIPCHK(hipEventRecord(done[k], st[k]));
+		HIPCHK(hipMemcpyAsync(verdicts + c, d->hs_dv[k], m, hipMemcpyDeviceToHost, d->hs_st[k]));
+		HIPCHK(hipEventRecord(d->hs_done[k], d->hs_st[k]));
 	}
-	HIPCHK(hipStreamSynchronize(st[0]));
-	HIPCHK(hipStreamSynchronize(st[1]));
+	HIPCHK(hipStreamSynchronize(d->hs_st[0]));
+	HIPCHK(hipStreamSynchronize(d->hs_st[1]));
 fail:
-	for (int k = 0; k < 2; k++) {
-		if (st[k]) hipStreamSynchronize(st[k]);
-		hipHostFree(hbuf[k]);
-		hipHostFree(hl[k]);
-		hipFree(dbuf[k]);
-		hipFree(dl[k]);
-		hipFree(dv[k]);
-		if (done[k]) hipEventDestroy(done[k]);
-		if (st[k]) hipStreamDestroy(st[k]);
-	}
 	return err;
 }
 
