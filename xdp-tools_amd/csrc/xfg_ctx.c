@@ -1146,6 +1146,14 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			a.spec = 0;
 		}
 	}
+	/* small rule sets: a direct LDS counter per hash-map slot (their few
+	 * counters are hot: more than the LDS counter cache holds) */
+	if (!a.pipe && !a.streamed && !a.variant && !a.hlog && !(cm && !strcmp(cm, "atomic"))) {
+		if (a.gbase[3] <= XFG_DCNT_MAX)
+			a.dcnt = a.gbase[3];       /* every hash-map counter */
+		else if (a.gbase[1] <= XFG_DCNT_MAX)
+			a.dcnt = a.gbase[1];       /* the IPv4 map's counters */
+	}
 	if (user && user != (void *)d->stream) {
 		HIPCHK(hipEventRecord(d->ev_user, (hipStream_t)user));
 		HIPCHK(hipStreamWaitEvent(d->stream, d->ev_user, 0));

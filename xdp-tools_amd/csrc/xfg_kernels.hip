@@ -823,6 +823,8 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 	if (a.hlog)
 		for (uint32_t i = tid; i < a.hlog_parts; i += TILE)
 			s_pcnt[i] = 0;
+	for (uint32_t i = tid; i < a.dcnt; i += TILE)   // (s_pcnt holds the direct counters)
+		s_pcnt[i] = 0;
 	if constexpr (PORTS) {
 		if (a.port_count)
 			for (int i = tid; i < 2048; i += TILE)
@@ -970,7 +972,9 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 				const unsigned long long same = __ballot(mine);
 				if (lane == leader) {
 					const uint32_t cnt = (uint32_t)__popcll(same);
-					if (!cache_hit(s_ctag, s_ccnt, lt, cnt)) {
+					if (lt < a.dcnt)
+						atomicAdd(&s_pcnt[lt], cnt);
+					else if (!cache_hit(s_ctag, s_ccnt, lt, cnt)) {
 						if (cnt > 1)
 							atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
 						else
@@ -981,7 +985,9 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 					tag = CT_NONE;
 			}
 		}
-		if (tag != CT_NONE && !cache_hit(s_ctag, s_ccnt, tag, 1))
+		if (tag != CT_NONE && tag < a.dcnt)
+			atomicAdd(&s_pcnt[tag], 1u);
+		else if (tag != CT_NONE && !cache_hit(s_ctag, s_ccnt, tag, 1))
 			cold_bump(a, s_pcnt, tag);
 
 		// 5. per-action stats (xdp_stats_record_action), kept per lane
@@ -1030,6 +1036,9 @@ __global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(con
 		for (uint32_t p = tid; p < a.hlog_parts; p += TILE)
 			a.hlog_cnt[(uint64_t)p * gridDim.x + blockIdx.x] =
 				s_pcnt[p] < a.hlog_cap ? s_pcnt[p] : a.hlog_cap;
+	for (uint32_t i = tid; i < a.dcnt; i += TILE)
+		if (s_pcnt[i])
+			atomicAdd(global_counter(a, i), (unsigned long long)s_pcnt[i]);
 }
 
 // ---------------------------------------------------------------- streamed kernel
@@ -1483,7 +1492,7 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 		hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
 		return hipGetLastError();
 	}
-	const size_t dl = a.hlog ? a.hlog_parts * 4 : 0;   // classic kernel's s_pcnt
+	const size_t dl = a.hlog ? a.hlog_parts * 4 : a.dcnt * 4;   // classic kernel's s_pcnt
 	if (a.streamed) {
 		hipLaunchKernelGGL((xfg_classify_stream_kernel<FEAT, 0>), dim3(grid), dim3(IO_THREADS), 0, s, a);
 		return hipGetLastError();

@@ -67,6 +67,7 @@
 
 #define XFG_HLOG_SHIFT    14u     /* hit-log partition: 16384 counters (64 KiB of LDS) */
 #define XFG_HLOG_PARTS_MAX 4096u  /* partitions a classify workgroup can track */
+#define XFG_DCNT_MAX      4096u   /* direct LDS counters (16 KiB) */
 #define XFG_SLOG_SHIFT    10u     /* speculative records: 1024 bucket lines per partition */
 
 
@@ -137,6 +138,10 @@ struct xfg_kargs {
 	uint32_t *hlog_cnt;
 	uint32_t hlog_cap;
 	uint32_t hlog_parts;
+	/* Classic kernel, small rule sets: the counters with identity < dcnt
+	 * (all hash maps, gbase[3], or the IPv4 map, gbase[1]) have a direct LDS
+	 * slot per workgroup, flushed once; 0 = off */
+	uint32_t dcnt;
 	/* Speculative single-lookup mode (xfg_spec.hip): 16-byte records per
 	 * (partition of 2^XFG_SLOG_SHIFT home buckets, workgroup), same layout
 	 * as the hit log; spec = 0 when the rule set has more than one live
