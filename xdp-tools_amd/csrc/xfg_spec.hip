@@ -137,29 +137,31 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 			cold(tag);
 	};
 	auto tile_of = [&](uint32_t k) -> uint32_t { return gw + k * nw; };
+	// Every lane loads unconditionally (addresses past the batch end are
+	// clamped to its last packet): a fixed number of loads per iteration
+	// lets the compiler's waits count exactly, instead of draining to
+	// vmcnt(0) where a load may or may not have been issued.
 	auto load_win = [&](uint32_t t, u32x4 (&w)[CPP], uint32_t &wl) {
 		const uint32_t base = t * 64;
 		const uint32_t rem = n - base >= 64u ? 64u : n - base;
 		if constexpr (DENSE) {
-			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + lane;
-		// (no zero fill: a register write behind a load still in flight
-		// would wait for it; lanes past the batch end are never parsed)
+			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W);
 #pragma unroll
-			for (int it = 0; it < CPP; it++)
-				if ((uint32_t)(it * 64 + lane) / CPP < rem)
-					w[it] = __builtin_nontemporal_load(src + it * 64);
+			for (int it = 0; it < CPP; it++) {
+				const uint32_t c = it * 64 + lane;
+				w[it] = __builtin_nontemporal_load(src + (c < rem * CPP ? c : rem * CPP - 1));
+			}
 		} else {
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
 				const int c = it * 64 + lane;
 				const uint32_t pk = c / CPP, sub = c % CPP;
-				if (pk < rem)
-					w[it] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
-						a.data + (uint64_t)(base + pk) * a.stride + sub * 16));
+				const uint32_t pc = pk < rem ? pk : rem - 1;
+				w[it] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
+					a.data + (uint64_t)(base + pc) * a.stride + sub * 16));
 			}
 		}
-		if ((uint32_t)lane < rem)
-			wl = load_len(a, base + lane);
+		wl = load_len(a, base + ((uint32_t)lane < rem ? (uint32_t)lane : rem - 1));
 	};
 
 	// Two window buffers and two S1 -> S2 state sets alternate roles: tile
@@ -184,6 +186,8 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 	if (my_nt > 1)
 		load_win(tile_of(1), W1.w, W1.len);
 
+	const unsigned long long *const bloom_base =
+		a.t4.bloom_words ? a.t4.bloom : reinterpret_cast<const unsigned long long *>(a.stats);
 	auto body = [&](uint32_t i, Win &Wc, const S12 &Sp, S12 &Sn) {
 		const bool s1 = i < my_nt, s2 = i >= 1;
 		// ------------------------------------------------ S1 (tile i)
@@ -195,6 +199,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 		Sn.key = 0;
 		Sn.h = 0;
 		bool df = false;
+		uint32_t bwi = 0;   // Bloom word of this lane's key (0: a word nobody needs)
 		const uint32_t gi1 = tile_of(i) * 64 + lane;
 		if (s1) {
 			__builtin_amdgcn_wave_barrier();
@@ -237,15 +242,17 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 							Sn.inf |= 16;
 							Sn.h = xfg_hash_v4(Sn.key, a.t4.seed);
 							if (a.t4.bloom_words)
-								Sn.bw = a.t4.bloom[xfg_bloom_word(Sn.h, a.t4.bloom_words)];
+								bwi = xfg_bloom_word(Sn.h, a.t4.bloom_words);
 						}
 					}
 				}
 			}
 		}
+		// one Bloom load per lane, always issued (see load_win)
+		Sn.bw = bloom_base[bwi];
 		// ------------------------------------------------ windows of tile i+2
-		if (i + 2 < my_nt)
-			load_win(tile_of(i + 2), Wc.w, Wc.len);
+		// (clamped to the wave's last tile: a fixed load count per iteration)
+		load_win(tile_of(i + 2 < my_nt ? i + 2 : (my_nt ? my_nt - 1 : 0)), Wc.w, Wc.len);
 		// ------------------------------------------------ S2 (tile i-1)
 		uint32_t act = A_NONE, tag = CT_NONE;
 		bool fk = false;
@@ -298,7 +305,9 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(W == 64 ? 
 			count_stats(act, Sp.len);
 		}
 	};
-	for (uint32_t i = 0; i < my_nt + 1; i += 2) {
+	// (a wave without tiles must not enter: its clamped loads would read
+	// past the batch)
+	for (uint32_t i = 0; my_nt && i < my_nt + 1; i += 2) {
 		body(i, W0, X1, X0);
 		if (i + 1 < my_nt + 1)
 			body(i + 1, W1, X0, X1);
