@@ -91,6 +91,7 @@ struct xfg_dev {
 
 struct xfg_ctx {
 	pthread_mutex_t lock;
+	pthread_mutex_t host_lock;      /* xfg_classify_host: the devices' staging buffers */
 	uint32_t prog_features;
 	const char *prog_name;
 	int ndev;
@@ -301,6 +302,7 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 	if (!ctx)
 		return -ENOMEM;
 	pthread_mutex_init(&ctx->lock, NULL);
+	pthread_mutex_init(&ctx->host_lock, NULL);
 	err = xfg_select_program(opts->features, &ctx->prog_name, &ctx->prog_features);
 	if (err)
 		goto fail;
@@ -387,6 +389,7 @@ void xfg_close(xfg_ctx *ctx)
 	free(ctx->port_flags_host);
 	free(ctx->port_bits_host);
 	pthread_mutex_destroy(&ctx->lock);
+	pthread_mutex_destroy(&ctx->host_lock);
 	free(ctx);
 }
 
@@ -1452,6 +1455,7 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t 
 		stride = b->stride;
 	size_t chunk_bytes = (size_t)HOST_CH * stride;
 
+	pthread_mutex_lock(&ctx->host_lock);   /* the staging buffers are shared */
 	HIPCHK(hipSetDevice(d->ordinal));
 	if ((err = host_staging(d, chunk_bytes)))
 		goto fail;
@@ -1480,6 +1484,10 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t 
 	HIPCHK(hipStreamSynchronize(d->hs_st[0]));
 	HIPCHK(hipStreamSynchronize(d->hs_st[1]));
 fail:
+	for (int k = 0; k < 2; k++)   /* (after an error: nothing may still use them) */
+		if (d->hs_st[k])
+			hipStreamSynchronize(d->hs_st[k]);
+	pthread_mutex_unlock(&ctx->host_lock);
 	return err;
 }
 
