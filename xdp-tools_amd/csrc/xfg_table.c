@@ -11,6 +11,9 @@
 static uint32_t buckets_for(uint32_t capacity, uint32_t spb)
 {
 	double lf = spb >= 12 ? 0.6 : (spb >= 6 ? 0.55 : 0.45);
+	const char *e = spb >= 12 ? getenv("XFG_LF4") : NULL;   /* diagnostics only */
+	if (e && atof(e) > 0.1 && atof(e) < 0.95)
+		lf = atof(e);
 	uint64_t nb = (uint64_t)((double)capacity / (spb * lf)) + 1;
 	if (nb > 0x7fffffffull / spb - 1)
 		nb = 0x7fffffffull / spb - 1;
