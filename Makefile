@@ -6,7 +6,10 @@
 # `make ref` additionally builds oracle/_ref/ from /root/reference (container only).
 JOBS ?= 8
 
-all: product synth oracle
+all: product synth oracle diag
+
+diag:
+	$(MAKE) -C xdp-tools_amd diag
 
 product:
 	$(MAKE) -C xdp-tools_amd -j$(JOBS)
@@ -27,4 +30,4 @@ clean:
 	$(MAKE) -C oracle clean
 	rm -f tools/libxfsynth.so
 
-.PHONY: all product synth oracle ref clean
+.PHONY: all product synth oracle ref diag clean

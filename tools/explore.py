@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
-"""tools/explore.py — classify-kernel time across workload shapes (diagnostic).
+"""tools/explore.py — classify time across workload shapes and measurement
+knobs (diagnostic; loads the diagnostics build of the library).
 
-Each scenario is 'rules:dst_permille:port_permille[:K=V,...]' (env knobs as in
-tools/ablate.py); the workload is bench.py's C3 generator with those
-parameters.  Prints one JSON line per scenario (median/min ms over rounds).
+Each scenario is 'rules:dst_permille:port_permille[:K=V,...]'; the workload is
+bench.py's C3 generator with those parameters.  Knobs (read by the
+diagnostics build only): XFG_KERNEL=general (the general kernel instead of
+the pipelined one), XFG_COUNT=atomic (no hit log), XFG_EMPTY=1 (tables
+treated as empty: stream + parse only), XFG_GRID_PER_CU=n, XFG_DIAG_MASK=m
+(IPv4-key kernel: 1 no counter bumps, 2 no bucket lines, 4 no Bloom loads, 8 no
+verdict stores; results wrong).
+Prints one JSON line per scenario (median/min ms over rounds).
 """
 import argparse
 import json
 import os
 import sys
 
+os.environ["XFG_LIB"] = "diag"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -17,7 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "xdp-tools_amd", "python"))
 
 import bench  # noqa: E402
 
-KNOBS = ("XFG_ABLATE", "XFG_VARIANT", "XFG_GRID_PER_CU", "XFG_KERNEL", "XFG_COUNT", "XFG_SPEC")
+KNOBS = ("XFG_KERNEL", "XFG_COUNT", "XFG_EMPTY", "XFG_GRID_PER_CU", "XFG_DIAG_MASK")
 
 
 def main():

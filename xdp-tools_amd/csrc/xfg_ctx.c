@@ -31,18 +31,18 @@ int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a, unsig
 			void *stream);
 int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sink, unsigned grid,
 			   void *stream);
-int xfg_classify_occupancy(uint32_t prog_features, uint32_t window);
+int xfg_classify_occupancy(uint32_t prog_features, int kind, uint32_t window, size_t dyn);
+int xfg_classify_threads(int kind, uint32_t window);
 int xfg_launch_compact(const uint8_t *verdicts, uint64_t n, uint32_t action, uint32_t *idx,
 		       unsigned long long *count, unsigned long long *status, uint32_t *ticket,
 		       unsigned grid, void *stream);
 uint64_t xfg_compact_tiles(uint64_t n);
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
-#define PORT_BITS_WORDS (XFG_PORT_MAP_ENTRIES / 32)
 
 struct dev_map {           /* device arrays of one hash map */
 	uint8_t *buckets;      /* (nbuckets + 1) * 64 B: keys, per-device flags, meta */
-	unsigned long long *bloom;
+	uint32_t *bloom;
 	unsigned long long *hits;
 	unsigned long long *red_hits; /* reduction copy (multi-process) */
 };
@@ -54,35 +54,34 @@ struct xfg_dev {
 	hipEvent_t ev0, ev1;
 	struct dev_map m[NMAPS_HASH];
 	uint8_t *port_flags;
-	uint32_t *port_bits;
 	unsigned long long *port_hits;
 	unsigned long long *red_port_hits;
 	unsigned long long *stats;      /* 10 */
 	unsigned long long *red_stats;  /* 10 */
 	void *sink;                     /* stream-read probe sink */
-	unsigned long long *prof;       /* diagnostics: XFG_PROF_WG x 8 phase cycles */
 	/* port table (xfg_layout.h): host mirror of this device's port flag
 	 * bytes, rebuilt into port_tab before a launch when dirty */
 	uint8_t *port_flags_h;
-	uint32_t *port_tab;
+	uint32_t *port_tab;             /* XFG_PORT_TAB entries (ruled ports <= XFG_PORT_TAB_MAX) */
+	uint32_t *port_nib;             /* XFG_PORT_NIB_WORDS (more ruled ports) */
 	uint32_t port_tab_disp;
 	int port_tab_ok, port_tab_dirty;
-	int occ64, occ128, occ_st;      /* resident classify workgroups per CU */
-	int occ_p64, occ_p128;          /* the same for the pipelined kernel */
-	int occ_s64;                    /* the speculative kernel (64-byte window) */
-	void *slog;                     /* speculative records */
-	uint32_t *slog_cnt;
-	uint64_t slog_bytes, slog_cnt_bytes;
+	/* resident classify workgroups per CU: [kernel: 0 general, 1 pipelined,
+	 * 2 pipelined IPv4-key mode][window 64, 128][dynamic LDS: none, direct
+	 * counters, port nibble map, both] */
+	int occ[3][2][4];
 	/* host-resident classify: persistent double-buffered staging */
 	uint8_t *hs_hbuf[2], *hs_dbuf[2], *hs_dv[2];
 	uint32_t *hs_hl[2], *hs_dl[2];
 	hipStream_t hs_st[2];
 	hipEvent_t hs_done[2];
 	size_t hs_bytes;
-	uint32_t *fix;                  /* pipelined kernel: deferred-packet lists */
-	uint64_t fix_bytes;
-	uint32_t *hlog, *hlog_cnt;      /* pipelined kernel: hit log */
-	uint64_t hlog_bytes, hlog_cnt_bytes;
+	pthread_mutex_t lock;           /* launch scratch below + compaction scratch */
+	int lock_ok;
+	uint32_t *defer;                /* pipelined kernel: deferred-packet lists */
+	uint64_t defer_bytes;
+	uint32_t *tlog, *pbuf, *pfill;  /* hit log: wave regions, partition buffers, fills */
+	uint64_t tlog_bytes, pbuf_bytes;
 	unsigned long long *cstatus;    /* verdict compaction: tile status words */
 	uint64_t cstatus_cap;
 	uint32_t *cticket;
@@ -101,7 +100,6 @@ struct xfg_ctx {
 	uint64_t *host_vals[NMAPS_HASH];
 	uint64_t *host_port_vals;
 	uint8_t *port_flags_host;        /* OR over devices of the port flags */
-	uint32_t *port_bits_host;        /* bit set <=> port_flags_host != 0 */
 	uint32_t port_count;
 	/* flag-bit census: flag_or[map][slot] = OR over devices of the slot's
 	 * flag byte; flag_cnt[map][bit] = slots with that bit (likewise for the
@@ -187,6 +185,10 @@ static int keylen_of(int map)
 /* ------------------------------------------------------------------ open */
 static void dev_free(struct xfg_dev *d)
 {
+	if (d->lock_ok) {
+		pthread_mutex_destroy(&d->lock);
+		d->lock_ok = 0;
+	}
 	if (hipSetDevice(d->ordinal) != hipSuccess)
 		return;
 	for (int i = 0; i < NMAPS_HASH; i++) {
@@ -196,13 +198,12 @@ static void dev_free(struct xfg_dev *d)
 		hipFree(d->m[i].red_hits);
 	}
 	hipFree(d->port_flags);
-	hipFree(d->port_bits);
+	hipFree(d->port_nib);
 	hipFree(d->port_hits);
 	hipFree(d->red_port_hits);
 	hipFree(d->stats);
 	hipFree(d->red_stats);
 	hipFree(d->sink);
-	hipFree(d->prof);
 	hipFree(d->port_tab);
 	free(d->port_flags_h);
 	hipFree(d->cstatus);
@@ -219,11 +220,10 @@ static void dev_free(struct xfg_dev *d)
 		if (d->hs_st[k])
 			hipStreamDestroy(d->hs_st[k]);
 	}
-	hipFree(d->fix);
-	hipFree(d->hlog);
-	hipFree(d->hlog_cnt);
-	hipFree(d->slog);
-	hipFree(d->slog_cnt);
+	hipFree(d->defer);
+	hipFree(d->tlog);
+	hipFree(d->pbuf);
+	hipFree(d->pfill);
 	hipFree(d->cticket);
 	if (d->ev_user)
 		hipEventDestroy(d->ev_user);
@@ -242,6 +242,8 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	int err = 0;
 	hipDeviceProp_t prop;
 
+	pthread_mutex_init(&d->lock, NULL);
+	d->lock_ok = 1;
 	HIPCHK(hipSetDevice(d->ordinal));
 	HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
 	d->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
@@ -252,22 +254,20 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 		const struct xfg_table *t = &ctx->t[i];
 		size_t ns = (size_t)t->nslots + 1;
 		HIPCHK(hipMalloc((void **)&d->m[i].buckets, xfg_table_img_bytes(t)));
-		HIPCHK(hipMalloc((void **)&d->m[i].bloom, (size_t)t->bloom_words * 8));
+		HIPCHK(hipMalloc((void **)&d->m[i].bloom, (size_t)t->bloom_words * 4));
 		HIPCHK(hipMalloc((void **)&d->m[i].hits, ns * 8));
 		HIPCHK(hipMemset(d->m[i].buckets, 0, xfg_table_img_bytes(t)));
-		HIPCHK(hipMemset(d->m[i].bloom, 0, (size_t)t->bloom_words * 8));
+		HIPCHK(hipMemset(d->m[i].bloom, 0, (size_t)t->bloom_words * 4));
 		HIPCHK(hipMemset(d->m[i].hits, 0, ns * 8));
 	}
 	HIPCHK(hipMalloc((void **)&d->port_flags, XFG_PORT_MAP_ENTRIES));
-	HIPCHK(hipMalloc((void **)&d->port_bits, PORT_BITS_WORDS * 4));
+	HIPCHK(hipMalloc((void **)&d->port_nib, XFG_PORT_NIB_WORDS * 4));
 	HIPCHK(hipMalloc((void **)&d->port_hits, XFG_PORT_MAP_ENTRIES * 8));
 	HIPCHK(hipMemset(d->port_flags, 0, XFG_PORT_MAP_ENTRIES));
-	HIPCHK(hipMemset(d->port_bits, 0, PORT_BITS_WORDS * 4));
 	HIPCHK(hipMemset(d->port_hits, 0, XFG_PORT_MAP_ENTRIES * 8));
 	HIPCHK(hipMalloc((void **)&d->stats, 10 * 8));
 	HIPCHK(hipMemset(d->stats, 0, 10 * 8));
 	HIPCHK(hipMalloc(&d->sink, 16 * 65536));
-	HIPCHK(hipMalloc((void **)&d->prof, XFG_PROF_WG * 8 * 8));
 	HIPCHK(hipMalloc((void **)&d->port_tab, XFG_PORT_TAB * 4));
 	d->port_flags_h = calloc(XFG_PORT_MAP_ENTRIES, 1);
 	if (!d->port_flags_h) {
@@ -275,15 +275,14 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 		goto fail;
 	}
 	d->port_tab_dirty = 1;
-	HIPCHK(hipMemset(d->prof, 0, XFG_PROF_WG * 8 * 8));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
-	d->occ64 = xfg_classify_occupancy(ctx->prog_features, 64);
-	d->occ128 = xfg_classify_occupancy(ctx->prog_features, 128);
-	d->occ_st = xfg_classify_occupancy(ctx->prog_features, 1);
-	d->occ_p64 = xfg_classify_occupancy(ctx->prog_features, 2);
-	d->occ_p128 = xfg_classify_occupancy(ctx->prog_features, 3);
-	d->occ_s64 = xfg_classify_occupancy(ctx->prog_features, 4);
+	for (int k = 0; k < 3; k++)
+		for (int w = 0; w < 2; w++)
+			for (int c = 0; c < 4; c++)
+				d->occ[k][w][c] = xfg_classify_occupancy(
+					ctx->prog_features, k, w ? 128 : 64,
+					(c & 1 ? XFG_DCNT_MAX * 4 : 0) + (c & 2 ? XFG_PORT_NIB_WORDS * 4 : 0));
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -323,8 +322,7 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 		}
 	}
 	ctx->port_flags_host = calloc(XFG_PORT_MAP_ENTRIES, 1);
-	ctx->port_bits_host = calloc(PORT_BITS_WORDS, 4);
-	if (!ctx->port_flags_host || !ctx->port_bits_host) {
+	if (!ctx->port_flags_host) {
 		err = -ENOMEM;
 		goto fail;
 	}
@@ -387,7 +385,6 @@ void xfg_close(xfg_ctx *ctx)
 	}
 	free(ctx->host_port_vals);
 	free(ctx->port_flags_host);
-	free(ctx->port_bits_host);
 	pthread_mutex_destroy(&ctx->lock);
 	pthread_mutex_destroy(&ctx->host_lock);
 	free(ctx);
@@ -511,8 +508,8 @@ static int push_bloom(xfg_ctx *ctx, int mi, int64_t word)
 	const struct xfg_table *t = &ctx->t[mi];
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
-		int err = word < 0 ? dev_write(d, d->m[mi].bloom, t->bloom, (size_t)t->bloom_words * 8)
-				   : dev_write(d, d->m[mi].bloom + word, t->bloom + word, 8);
+		int err = word < 0 ? dev_write(d, d->m[mi].bloom, t->bloom, (size_t)t->bloom_words * 4)
+				   : dev_write(d, d->m[mi].bloom + word, t->bloom + word, 4);
 		if (err)
 			return err;
 	}
@@ -539,7 +536,7 @@ static int port_key(const void *key, uint32_t *k)
 }
 
 /* Track which ports have any flag on any device: port_count (the empty-map
- * skip) and the 65536-bit bitmap the kernel stages in LDS. */
+ * skip) and the flag census. */
 static int port_flags_note(xfg_ctx *ctx, uint32_t k, uint8_t f)
 {
 	census(ctx->port_flag_cnt, ctx->port_flags_host[k], f);
@@ -548,19 +545,6 @@ static int port_flags_note(xfg_ctx *ctx, uint32_t k, uint8_t f)
 	else if (ctx->port_flags_host[k] && !f)
 		ctx->port_count--;
 	ctx->port_flags_host[k] = f;
-	uint32_t w = k / 32, before = ctx->port_bits_host[w];
-	if (f)
-		ctx->port_bits_host[w] |= 1u << (k % 32);
-	else
-		ctx->port_bits_host[w] &= ~(1u << (k % 32));
-	if (before == ctx->port_bits_host[w])
-		return 0;
-	for (int i = 0; i < ctx->ndev; i++) {
-		struct xfg_dev *d = &ctx->dev[i];
-		int err = dev_write(d, d->port_bits + w, ctx->port_bits_host + w, 4);
-		if (err)
-			return err;
-	}
 	return 0;
 }
 
@@ -906,7 +890,7 @@ static int update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t 
 		if (!e2)
 			e2 = dev_write(d, d->m[mi].hits, hits + ns * i, ns * 8);
 		if (!e2)
-			e2 = dev_write(d, d->m[mi].bloom, t->bloom, (size_t)t->bloom_words * 8);
+			e2 = dev_write(d, d->m[mi].bloom, t->bloom, (size_t)t->bloom_words * 4);
 		if (e2 && !err)
 			err = e2;
 	}
@@ -930,9 +914,10 @@ int xfg_map_update_batch_percpu(xfg_ctx *ctx, int map, const void *keys, const u
 }
 
 /* ------------------------------------------------------------------ classify */
-/* Rebuild a device's LDS port table from its flag bytes (linear probing from
- * xfg_port_slot()); with more than XFG_PORT_TAB_MAX ruled ports the kernel
- * uses the bitmap + port_flags path instead. */
+/* Rebuild a device's LDS port image from its flag bytes: the open-addressed
+ * table (linear probing from xfg_port_slot()) when at most XFG_PORT_TAB_MAX
+ * ports carry flags, else the nibble map of every port's low 4 flag bits
+ * (the only ones CHECK_MAP can test). */
 static int port_tab_refresh(struct xfg_dev *d)
 {
 	uint32_t tab[XFG_PORT_TAB];
@@ -957,9 +942,16 @@ static int port_tab_refresh(struct xfg_dev *d)
 	d->port_tab_ok = n <= XFG_PORT_TAB_MAX;
 	d->port_tab_disp = disp;
 	d->port_tab_dirty = 0;
-	if (!d->port_tab_ok)
-		return 0;
-	return dev_write(d, d->port_tab, tab, sizeof(tab));
+	if (d->port_tab_ok)
+		return dev_write(d, d->port_tab, tab, sizeof(tab));
+	uint32_t *nib = calloc(XFG_PORT_NIB_WORDS, 4);
+	if (!nib)
+		return -ENOMEM;
+	for (uint32_t k = 0; k < XFG_PORT_MAP_ENTRIES; k++)
+		nib[k >> 3] |= (uint32_t)(d->port_flags_h[k] & 15) << ((k & 7) * 4);
+	int err = dev_write(d, d->port_nib, nib, XFG_PORT_NIB_WORDS * 4);
+	free(nib);
+	return err;
 }
 
 static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b,
@@ -984,14 +976,12 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 		gb += (uint64_t)ctx->t[i].nslots + 1;
 	}
 	a->gbase[3] = (uint32_t)gb;
-	a->port_flags = d->port_flags;
-	a->port_bits = d->port_bits;
 	a->port_hits = d->port_hits;
 	a->port_count = ctx->port_count;
 	a->port_tab = d->port_tab_ok ? d->port_tab : NULL;
+	a->port_nib = d->port_nib;
 	a->port_tab_disp = d->port_tab_disp;
 	a->stats = d->stats;
-	a->prof = d->prof;
 	a->data = b->data;
 	a->offsets = b->offsets;
 	a->lens = b->lens;
@@ -1001,176 +991,139 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	a->verdicts = verdicts;
 	/* Header window: the fixed-stride 64-byte layout needs no more than its
 	 * stride; everything else stages 128 bytes (every synthetic class and all
-	 * common headers parse within 78 bytes; longer chains read HBM). */
+	 * common headers parse within 78 bytes; a longer parse reads HBM). */
 	a->window = (!b->offsets && b->stride && b->stride <= 64) ? 64 : 128;
-	/* The streamed kernel takes every fixed-stride batch whose 64-byte
-	 * windows and 16-byte length chunks can be DMA'd whole (headers past
-	 * byte 64 are read from HBM by the few packets that have them). */
-	a->streamed = !b->offsets && b->stride >= 64 && !((uintptr_t)b->lens & 15);
-	const char *ks = getenv("XFG_KERNEL");    /* diagnostics only */
-	if (!ks || strcmp(ks, "stream"))
-		a->streamed = 0;   /* experimental: opt-in until it beats the classic kernel */
-	if (a->streamed)
-		a->window = 64;
 	/* The pipelined kernel takes every fixed-stride batch whose windows can
-	 * be loaded without a length (stride >= window, 16-byte aligned). */
-	a->pipe = !a->streamed && !b->offsets && b->stride >= a->window && !(b->stride & 15) &&
+	 * be loaded without a length (stride >= window, 16-byte aligned; packet
+	 * indices fit its 32-bit deferred lists); the general kernel the rest. */
+	a->pipe = !b->offsets && b->stride >= a->window && !(b->stride & 15) &&
 		  !((uintptr_t)b->data & 15) && b->count < (1ull << 32);
-	if (!ks || strcmp(ks, "pipe"))
-		a->pipe = 0;   /* experimental: opt-in (XFG_KERNEL=pipe) until it beats the classic kernel */
-	/* Speculative single-lookup mode (xfg_spec.hip): IPv4 keys of one
-	 * direction only (census), no live Ethernet or IPv6 lookup. */
-	if (a->pipe && (ctx->prog_features & (1u << 3))) {
-		int v4d = (a->t4.fmask & 2) == 2, v4s = (a->t4.fmask & 1) == 1;
-		int eth_live = a->te.count && (a->te.fmask & 3);
-		int v6_live = a->t6.count && (a->t6.fmask & 3);
-		const char *sp = getenv("XFG_SPEC");   /* diagnostics: "0" disables */
-		a->spec = a->t4.count && v4d != v4s && !eth_live && !v6_live &&
-			  !(sp && !strcmp(sp, "0"));
+#ifdef XFG_DIAG
+	const char *ks = getenv("XFG_KERNEL");   /* diagnostics build only */
+	if (ks && !strcmp(ks, "general"))
+		a->pipe = 0;
+#endif
+	a->dense = a->pipe && a->stride == a->window;
+	/* key mode 1: no Ethernet or IPv6 lookup can hit (flag census), so the
+	 * pipelined kernel carries IPv4 keys only */
+	int eth_live = (ctx->prog_features & XFG_FEAT_ETHERNET) && a->te.count && (a->te.fmask & 3);
+	int v6_live = (ctx->prog_features & XFG_FEAT_IPV6) && a->t6.count && (a->t6.fmask & 3);
+	a->km = (ctx->prog_features & XFG_FEAT_IPV4) && !eth_live && !v6_live;
+	/* per-lane u32 byte sums in the pipelined kernel: bound them */
+	if (a->pipe && (uint64_t)a->stride * (((b->count + 63) / 64 + 1023) / 1024 + 1) >= (1ull << 32))
+		a->pipe = 0;
+#ifdef XFG_DIAG
+	const char *dm = getenv("XFG_DIAG_MASK");   /* pipelined IPv4-key kernel: drop a cost */
+	if (dm && *dm)
+		a->diag = (uint32_t)strtoul(dm, NULL, 0);
+	const char *em = getenv("XFG_EMPTY");   /* every table empty: stream + parse only */
+	if (em && !strcmp(em, "1")) {
+		a->t4.count = a->t6.count = a->te.count = 0;
+		a->port_count = 0;
 	}
-	/* Diagnostics only: XFG_ABLATE=<mask> (1 = treat every table as empty,
-	 * 2 = drop counter atomics, 4 = stage windows only).  Results are wrong
-	 * under any non-zero mask; tools/ablate.py uses it to split time. */
-	const char *mw = getenv("XFG_VARIANT");
-	if (mw && *mw)
-		a->variant = (uint32_t)strtoul(mw, NULL, 0);
-	const char *ab = getenv("XFG_ABLATE");
-	if (ab && *ab) {
-		a->ablate = (uint32_t)strtoul(ab, NULL, 0);
-		if (a->ablate & 1) {
-			a->spec = 0;
-			a->t4.count = a->t6.count = a->te.count = 0;
-			a->port_count = 0;
-		}
-	}
-	a->dense = !a->offsets && !a->descs && a->stride == a->window;
+#endif
 	return 0;
 }
 
-/* One persistent wave of workgroups: every resident slot of every CU. */
-static unsigned grid_for(const struct xfg_dev *d, const struct xfg_kargs *a)
+/* Device scratch buffer of at least @bytes (grown on demand; the old one may
+ * still be in use by a launch queued on the device stream: wait for it). */
+static int scratch(struct xfg_dev *d, void **p, uint64_t *have, uint64_t bytes)
 {
-	uint64_t tiles = (a->n + 255) / 256;   /* pipelined: 4 waves x 64 packets */
-	uint64_t per_cu = a->streamed ? d->occ_st
-			: a->pipe ? (a->window <= 64 ? (a->spec ? d->occ_s64 : d->occ_p64) : d->occ_p128)
-			: a->window <= 64 ? d->occ64 : d->occ128;
-	const char *g = getenv("XFG_GRID_PER_CU");   /* diagnostics only */
-	if (g && *g)
-		per_cu = strtoul(g, NULL, 0);
-	uint64_t cap = (uint64_t)d->ncu * (per_cu ? per_cu : 4);
-	if (tiles > cap)
-		tiles = cap;
-	return tiles ? (unsigned)tiles : 1;
+	if (bytes <= *have)
+		return 0;
+	int err = hip_err(hipStreamSynchronize(d->stream));
+	if (err)
+		return err;
+	hipFree(*p);
+	*p = NULL;
+	*have = 0;
+	err = hip_err(hipMalloc(p, bytes));
+	if (!err)
+		*have = bytes;
+	return err;
 }
 
 /* classify launches on the device's own stream (every classify of a device
  * is serialised there), ordered after and before @user (a caller's stream,
- * or NULL). */
+ * or NULL).  The per-launch scratch (hit log, deferred lists) is sized and
+ * used under the device lock, so concurrent callers never see a buffer
+ * being replaced. */
 static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs *a0,
 			void *user, int iters)
 {
 	int err = 0;
 	struct xfg_kargs a = *a0;
-	unsigned grid = grid_for(d, &a);
-	if (a.pipe) {
-		/* one list per wave, room for every packet of its tiles */
-		uint64_t nw = (uint64_t)grid * 4, nt = (a.n + 63) / 64;
-		uint64_t cap = (nt + nw - 1) / nw * 64;
-		uint64_t bytes = nw * (cap ? cap : 64) * 4;
-		if (bytes > d->fix_bytes) {
-			hipFree(d->fix);
-			d->fix = NULL;
-			d->fix_bytes = 0;
-			HIPCHK(hipMalloc((void **)&d->fix, bytes));
-			d->fix_bytes = bytes;
-		}
-		a.fix_list = d->fix;
-		a.fix_cap = (uint32_t)cap;
-	}
-	/* hit log (pipelined kernels, and the classic kernel's production build):
-	 * room for twice a uniform share of the workgroup's packets in each
-	 * partition (a fuller region spills to atomics) */
-	uint64_t parts = ((uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES + (1u << XFG_HLOG_SHIFT) - 1) >>
-			 XFG_HLOG_SHIFT;
-	const char *cm = getenv("XFG_COUNT");   /* diagnostics: "atomic" | "log" */
-	int any = a.t4.count || a.t6.count || a.te.count || a.port_count;
-	/* (measured on C3: the classic kernel is faster with atomics, 0.467 ms
-	 * against 0.51 with the log, so there the log is opt-in) */
-	if (!a.streamed && (a.pipe || (!a.variant && cm && !strcmp(cm, "log")))) {
-		if (any && parts <= XFG_HLOG_PARTS_MAX && !(cm && !strcmp(cm, "atomic"))) {
-			uint64_t per_wg = (a.n + grid - 1) / grid;
-			uint64_t hcap = (2 * ((per_wg + parts - 1) / parts) + 32 + 3) & ~3ull;
-			uint64_t lb = parts * grid * hcap * 4, cb = parts * grid * 4;
-			if (lb > d->hlog_bytes) {
-				hipFree(d->hlog);
-				d->hlog = NULL;
-				d->hlog_bytes = 0;
-				HIPCHK(hipMalloc((void **)&d->hlog, lb));
-				d->hlog_bytes = lb;
-			}
-			if (cb > d->hlog_cnt_bytes) {
-				hipFree(d->hlog_cnt);
-				d->hlog_cnt = NULL;
-				d->hlog_cnt_bytes = 0;
-				HIPCHK(hipMalloc((void **)&d->hlog_cnt, cb));
-				d->hlog_cnt_bytes = cb;
-			}
-			a.hlog = d->hlog;
-			a.hlog_cnt = d->hlog_cnt;
-			a.hlog_cap = (uint32_t)hcap;
-			a.hlog_parts = (uint32_t)parts;
-		}
-		/* speculative records: twice a uniform share per (partition,
-		 * workgroup); a fuller region defers its packets to the serial pass */
-		uint64_t sparts = ((uint64_t)a.t4.nbuckets + 1 + (1u << XFG_SLOG_SHIFT) - 1) >> XFG_SLOG_SHIFT;
-		if (a.spec && sparts <= XFG_HLOG_PARTS_MAX) {
-			uint64_t per_wg = (a.n + grid - 1) / grid;
-			uint64_t scap = 2 * ((per_wg + sparts - 1) / sparts) + 16;
-			uint64_t lb = sparts * grid * scap * 16, cb = sparts * grid * 4;
-			if (lb > d->slog_bytes) {
-				hipFree(d->slog);
-				d->slog = NULL;
-				d->slog_bytes = 0;
-				HIPCHK(hipMalloc(&d->slog, lb));
-				d->slog_bytes = lb;
-			}
-			if (cb > d->slog_cnt_bytes) {
-				hipFree(d->slog_cnt);
-				d->slog_cnt = NULL;
-				d->slog_cnt_bytes = 0;
-				HIPCHK(hipMalloc((void **)&d->slog_cnt, cb));
-				d->slog_cnt_bytes = cb;
-			}
-			a.slog = d->slog;
-			a.slog_cnt = d->slog_cnt;
-			a.slog_cap = (uint32_t)scap;
-			a.slog_parts = (uint32_t)sparts;
-		} else {
-			a.spec = 0;
-		}
-	}
+	const int kind = a.pipe ? (a.km ? 2 : 1) : 0, wi = a.window > 64;
+	const char *cm = NULL;
+#ifdef XFG_DIAG
+	cm = getenv("XFG_COUNT");   /* diagnostics build only: "atomic" */
+#endif
 	/* small rule sets: a direct LDS counter per hash-map slot (their few
 	 * counters are hot: more than the LDS counter cache holds) */
-	if (!a.pipe && !a.streamed && !a.variant && !a.hlog && !(cm && !strcmp(cm, "atomic"))) {
-		if (a.gbase[3] <= XFG_DCNT_MAX)
-			a.dcnt = a.gbase[3];       /* every hash-map counter */
-		else if (a.gbase[1] <= XFG_DCNT_MAX)
-			a.dcnt = a.gbase[1];       /* the IPv4 map's counters */
+	if (a.gbase[3] <= XFG_DCNT_MAX)
+		a.dcnt = a.gbase[3];       /* every hash-map counter */
+	else if (a.gbase[1] <= XFG_DCNT_MAX)
+		a.dcnt = a.gbase[1];       /* the IPv4 map's counters */
+	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
+#ifdef XFG_DIAG
+	const char *g = getenv("XFG_GRID_PER_CU");
+	if (g && *g)
+		per_cu = (int)strtol(g, NULL, 0);
+#endif
+	const uint64_t per_wg = (uint64_t)xfg_classify_threads(kind, a.window);
+	uint64_t grid = (uint64_t)d->ncu * (per_cu > 0 ? per_cu : 1);
+	uint64_t need = (a.n + per_wg - 1) / per_wg;
+	if (grid > need)
+		grid = need ? need : 1;
+
+	pthread_mutex_lock(&d->lock);
+	if (a.pipe) {
+		/* one deferred list per wave, room for every packet of its tiles */
+		uint64_t nw = grid * (per_wg / 64), nt = (a.n + 63) / 64;
+		uint64_t cap = (nt + nw - 1) / nw * 64;
+		if ((err = scratch(d, (void **)&d->defer, &d->defer_bytes, nw * cap * 4)))
+			goto out;
+		a.defer = d->defer;
+		a.defer_cap = (uint32_t)cap;
+	}
+	/* hit log (pipelined kernels): the hash-map counters without a direct
+	 * LDS counter, when the count kernel's histogram covers them; the wave
+	 * regions share the deferred lists' bound, the partition buffers hold
+	 * twice a uniform share (a fuller one spills to atomics) */
+	uint64_t total = (uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES;
+	uint64_t hist = ((total + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
+	int logged = a.t4.count || a.t6.count || a.te.count;
+	if (a.pipe && logged && a.dcnt < a.gbase[3] && hist <= XFG_LOG_HIST_MAX &&
+	    !(cm && !strcmp(cm, "atomic"))) {
+		uint64_t pcap = 2 * ((a.n + XFG_LOG_PARTS - 1) / XFG_LOG_PARTS) + 1024;
+		if ((err = scratch(d, (void **)&d->tlog, &d->tlog_bytes,
+				   grid * (per_wg / 64) * (uint64_t)a.defer_cap * 4)) ||
+		    (err = scratch(d, (void **)&d->pbuf, &d->pbuf_bytes, XFG_LOG_PARTS * pcap * 4)))
+			goto out;
+		if (!d->pfill) {
+			if ((err = hip_err(hipMalloc((void **)&d->pfill, XFG_LOG_PARTS * 4))) ||
+			    (err = hip_err(hipMemset(d->pfill, 0, XFG_LOG_PARTS * 4))))
+				goto out;
+		}
+		a.tlog = d->tlog;
+		a.pbuf = d->pbuf;
+		a.pfill = d->pfill;
+		a.pcap = (uint32_t)pcap;
+		a.log_hist = (uint32_t)hist;
 	}
 	if (user && user != (void *)d->stream) {
-		HIPCHK(hipEventRecord(d->ev_user, (hipStream_t)user));
-		HIPCHK(hipStreamWaitEvent(d->stream, d->ev_user, 0));
+		if ((err = hip_err(hipEventRecord(d->ev_user, (hipStream_t)user))) ||
+		    (err = hip_err(hipStreamWaitEvent(d->stream, d->ev_user, 0))))
+			goto out;
 	}
-	for (int i = 0; i < iters; i++) {
-		if ((err = xfg_launch_classify(ctx->prog_features, &a, grid, d->stream)))
-			goto fail;
+	for (int i = 0; i < iters && !err; i++)
+		err = xfg_launch_classify(ctx->prog_features, &a, (unsigned)grid, d->stream);
+	if (!err && user && user != (void *)d->stream) {
+		if (!(err = hip_err(hipEventRecord(d->ev_done, d->stream))))
+			err = hip_err(hipStreamWaitEvent((hipStream_t)user, d->ev_done, 0));
 	}
-	if (user && user != (void *)d->stream) {
-		HIPCHK(hipEventRecord(d->ev_done, d->stream));
-		HIPCHK(hipStreamWaitEvent((hipStream_t)user, d->ev_done, 0));
-	}
-	return 0;
-fail:
+out:
+	pthread_mutex_unlock(&d->lock);
 	return err;
 }
 
@@ -1238,7 +1191,7 @@ int xfg_classify_descs(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *db,
 	a.desc_mask = db->mask;
 	a.desc_first = db->first;
 	a.window = 128;
-	a.streamed = 0;
+	a.pipe = 0;
 	a.dense = 0;
 	err = hip_err(hipSetDevice(d->ordinal));
 	if (!err)
@@ -1276,7 +1229,10 @@ fail:
 	return err;
 }
 
-/* Verdict compaction (include/xdpfilter_gpu.h). */
+/* Verdict compaction (include/xdpfilter_gpu.h).  The kernel uses per-device
+ * scratch (tile status words, ticket), so it runs on the device's own stream,
+ * ordered after and before the caller's stream: two compactions never
+ * overlap on one device, whatever streams their callers pass. */
 int xfg_compact(xfg_ctx *ctx, int dev, const uint8_t *verdicts, uint64_t n, uint32_t action,
 		uint32_t *idx, uint64_t *count, void *stream)
 {
@@ -1289,22 +1245,31 @@ int xfg_compact(xfg_ctx *ctx, int dev, const uint8_t *verdicts, uint64_t n, uint
 		return -EINVAL;
 	struct xfg_dev *d = &ctx->dev[dev];
 	uint64_t tiles = xfg_compact_tiles(n);
-	pthread_mutex_lock(&ctx->lock);
+	pthread_mutex_lock(&d->lock);
 	HIPCHK(hipSetDevice(d->ordinal));
 	if (!d->cticket)
 		HIPCHK(hipMalloc((void **)&d->cticket, 4));
 	if (tiles > d->cstatus_cap) {
+		HIPCHK(hipStreamSynchronize(d->stream));   /* the old buffer may be in use */
 		hipFree(d->cstatus);
 		d->cstatus = NULL;
 		d->cstatus_cap = 0;
 		HIPCHK(hipMalloc((void **)&d->cstatus, tiles * 8));
 		d->cstatus_cap = tiles;
 	}
-	hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+	hipStream_t user = (hipStream_t)stream;
+	if (user && user != d->stream) {
+		HIPCHK(hipEventRecord(d->ev_user, user));
+		HIPCHK(hipStreamWaitEvent(d->stream, d->ev_user, 0));
+	}
 	err = xfg_launch_compact(verdicts, n, action, idx, (unsigned long long *)count,
-				 d->cstatus, d->cticket, (unsigned)d->ncu * 4, s);
+				 d->cstatus, d->cticket, (unsigned)d->ncu * 4, d->stream);
+	if (!err && user && user != d->stream) {
+		HIPCHK(hipEventRecord(d->ev_done, d->stream));
+		HIPCHK(hipStreamWaitEvent(user, d->ev_done, 0));
+	}
 fail:
-	pthread_mutex_unlock(&ctx->lock);
+	pthread_mutex_unlock(&d->lock);
 	return err;
 }
 
@@ -1665,21 +1630,5 @@ int xfg_comm_allreduce(xfg_ctx *ctx)
 	ctx->reduced = 1;
 	return 0;
 fail:
-	return err;
-}
-
-/* Diagnostics: the per-workgroup phase cycles of the last profiled launch
- * (XFG_VARIANT=4), XFG_PROF_WG x 8 u64; the record is zeroed after reading. */
-int xfg_diag_prof(xfg_ctx *ctx, int dev, uint64_t *out, uint64_t n)
-{
-	if (!ctx || !out || dev < 0 || dev >= ctx->ndev)
-		return -EINVAL;
-	struct xfg_dev *d = &ctx->dev[dev];
-	uint64_t max = (uint64_t)XFG_PROF_WG * 8;
-	if (n > max)
-		n = max;
-	int err = dev_read(d, out, d->prof, n * 8);
-	if (!err)
-		err = hip_err(hipMemset(d->prof, 0, max * 8));
 	return err;
 }

@@ -45,13 +45,6 @@ constexpr uint32_t F_IPV6 = 1u << 2;
 constexpr uint32_t F_IPV4 = 1u << 3;
 constexpr uint32_t F_ETH = 1u << 4;
 constexpr uint32_t F_DENY = 1u << 6;
-// Diagnostics only (XFG_VARIANT >= 0x100 on the headline program): feature-
-// word bits that remove a code path to measure its instruction cost.
-// Results are wrong with any of them set.
-constexpr uint32_t X_NOGEN = 1u << 8;    // no generic parse (fast path or abort)
-constexpr uint32_t X_NOV6 = 1u << 9;     // no IPv6 / NDISC lookups
-constexpr uint32_t X_NOPORT = 1u << 10;  // no port lookups
-constexpr uint32_t X_NOCNT = 1u << 11;   // no counter bump code
 
 constexpr uint32_t M_SRC = 1, M_DST = 2, M_TCP = 4, M_UDP = 8;
 constexpr uint32_t A_ABORTED = 0, A_DROP = 1, A_PASS = 2, A_NONE = 7;
@@ -232,10 +225,6 @@ __device__ __forceinline__ Parsed parse(const P &p)
 	r.pdst = r.psrc = 0;
 	if (parse_fast<FEAT, W, P>(p, r))
 		return r;
-	if constexpr ((FEAT & X_NOGEN) != 0) {
-		r.abort_at = ST_ETH;
-		return r;
-	}
 	const uint32_t len = p.len;
 
 	// parse_ethhdr (parsing_helpers.h:100-134), VLAN_MAX_DEPTH 4
@@ -379,8 +368,8 @@ __device__ __forceinline__ const uint8_t *bucket_ptr(const xfg_tdesc &t, uint32_
 
 __device__ __forceinline__ bool bloom_maybe(const xfg_tdesc &t, uint32_t h)
 {
-	const unsigned long long w = t.bloom[xfg_bloom_word(h, t.bloom_words)];
-	const unsigned long long m = xfg_bloom_mask(h);
+	const uint32_t w = t.bloom[xfg_bloom_word(h, t.bloom_words)];
+	const uint32_t m = xfg_bloom_mask(h);
 	return (w & m) == m;
 }
 
@@ -560,22 +549,6 @@ __device__ __forceinline__ unsigned long long *global_counter(const xfg_kargs &a
 	return a.t4.hits + g;
 }
 
-// One cold counter bump: appended to the workgroup's region of its hit-log
-// partition (a plain store; xfg_hlog_count_kernel adds the regions up), or,
-// with no log or a full region, a memory-side atomic.
-__device__ __forceinline__ void cold_bump(const xfg_kargs &a, uint32_t *s_pcnt, uint32_t tag)
-{
-	if (a.hlog) {
-		const uint32_t p = tag >> XFG_HLOG_SHIFT;
-		const uint32_t pos = atomicAdd(&s_pcnt[p], 1u);
-		if (pos < a.hlog_cap) {
-			a.hlog[((uint64_t)p * gridDim.x + blockIdx.x) * a.hlog_cap + pos] = tag;
-			return;
-		}
-	}
-	atomicAdd(global_counter(a, tag), 1ull);
-}
-
 // CHECK_MAP (xdp-filter/xdpfilt_prog.h:56-64): hit iff the key exists and
 // (value & mask) == mask; the counter bump is deferred to the caller.
 __device__ __forceinline__ bool take(const Hit &h, uint32_t mask, uint32_t base, uint32_t &tag)
@@ -594,8 +567,10 @@ __device__ __forceinline__ bool can_hit(uint32_t fmask, uint32_t m)
 	return (fmask & m) == m;
 }
 
-// s_ports: the port table (kargs.port_tab) or, without one, the "any flag"
-// bitmap in front of a port_flags read.
+// s_ports: the workgroup's LDS copy of the ruled ports -- the open-addressed
+// table (kargs.port_tab, at most XFG_PORT_TAB_MAX ports) or, with more, the
+// 65536-entry nibble map of every port's flags (kargs.port_nib).  Only the
+// four flag bits CHECK_MAP can test (SRC|DST|TCP|UDP) are kept.
 __device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s_ports,
 					   uint32_t key, uint32_t mask, uint32_t &tag)
 {
@@ -615,9 +590,7 @@ __device__ __forceinline__ bool check_port(const xfg_kargs &a, const uint32_t *s
 			sl = (sl + 1) & (XFG_PORT_TAB - 1);
 		}
 	} else {
-		if (!((s_ports[key >> 5] >> (key & 31)) & 1))
-			return false;
-		f = a.port_flags[key];
+		f = (s_ports[key >> 3] >> ((key & 7) * 4)) & 15;
 	}
 	if ((f & mask) == mask) {
 		tag = a.gbase[3] + key;
@@ -675,7 +648,7 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, co
 				return HIT;
 		}
 	}
-	if constexpr ((FEAT & F_IPV6) != 0 && (FEAT & X_NOV6) == 0) {
+	if constexpr ((FEAT & F_IPV6) != 0) {
 		if (a.t6.count && r.l3 == 3) {
 			// lookup_verdict_ipv6: dst then src (xdpfilt_prog.h:152-165)
 			Probe<6, NT> d, s;
@@ -691,7 +664,7 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, co
 	}
 	if (r.abort_at == ST_ND)
 		return A_ABORTED;
-	if constexpr ((FEAT & F_IPV6) != 0 && (FEAT & X_NOV6) == 0) {
+	if constexpr ((FEAT & F_IPV6) != 0) {
 		if (a.t6.count && r.nd) {
 			// NDISC target: NS => DST, NA => SRC (xdpfilt_prog.h:277-285)
 			const uint32_t mt = r.nd == 135 ? M_DST : M_SRC;
@@ -705,7 +678,7 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, co
 	}
 	if (r.abort_at == ST_L4)
 		return A_ABORTED;
-	if constexpr ((FEAT & (F_UDP | F_TCP)) != 0 && (FEAT & X_NOPORT) == 0) {
+	if constexpr ((FEAT & (F_UDP | F_TCP)) != 0) {
 		if (a.port_count && r.l4proto) {
 			// lookup_verdict_udp / _tcp (xdpfilt_prog.h:92-101 / :76-85)
 			const uint32_t pm = r.l4proto == 17 ? M_UDP : M_TCP;
@@ -741,38 +714,17 @@ __device__ __forceinline__ bool cache_hit(uint32_t *s_ctag, uint32_t *s_ccnt, ui
 }
 
 
-// Diagnostics (build variant V & 4): per-workgroup cycles spent in each
-// phase of the tile loop, stamped by wave 0 and written to kargs.prof.
-constexpr int NPHASE = 8;
-struct Stamps {
-	unsigned long long last;
-	uint32_t *acc;   // LDS, NPHASE words
-	__device__ __forceinline__ void init(uint32_t *lds)
-	{
-		acc = lds;
-		if (threadIdx.x < NPHASE)
-			acc[threadIdx.x] = 0;
-		last = __builtin_amdgcn_s_memtime();
-	}
-	__device__ __forceinline__ void mark(int i)
-	{
-		const unsigned long long t = __builtin_amdgcn_s_memtime();
-		if (threadIdx.x == 0)
-			acc[i] += (uint32_t)(t - last);
-		last = t;
-	}
-	__device__ __forceinline__ void store(unsigned long long *prof) const
-	{
-		if (prof && threadIdx.x == 0 && blockIdx.x < XFG_PROF_WG)
-			for (int i = 0; i < NPHASE; i++)
-				prof[(uint64_t)blockIdx.x * NPHASE + i] = acc[i];
-	}
-};
-
 // Word w of packet i's AF_XDP descriptor (ring index wraps with desc_mask).
 __device__ __forceinline__ uint64_t desc_word(const xfg_kargs &a, uint64_t i, int w)
 {
 	return a.descs[2ull * ((a.desc_first + (uint32_t)i) & a.desc_mask) + w];
+}
+
+// Length of packet i in the pipelined kernels' layout (no descriptors).
+__device__ __forceinline__ uint32_t load_len_fixed(const xfg_kargs &a, uint32_t i)
+{
+	return a.lens_u16 ? static_cast<const uint16_t *>(a.lens)[i]
+			  : static_cast<const uint32_t *>(a.lens)[i];
 }
 
 __device__ __forceinline__ uint32_t load_len(const xfg_kargs &a, uint64_t i)
@@ -794,755 +746,372 @@ __device__ __forceinline__ const uint8_t *pkt_ptr(const xfg_kargs &a, uint64_t i
 	return a.data + (a.offsets ? a.offsets[i] : i * (uint64_t)a.stride);
 }
 
-// ---------------------------------------------------------------- the kernel
-// V: build variant bits (production = 0 unless measured better):
-//   1 = non-temporal bucket-line loads, 2 = ask the allocator for 5 waves/SIMD
-// DENSE: the batch is known to be the dense fixed-stride layout (stride == W,
-// no offsets/descriptors), so the stream loads need no per-packet address
-// or length: a separate build, as the general load path costs registers.
-template <uint32_t FEAT, int W, int V, bool DENSE = false>
-__global__ __launch_bounds__(TILE, (V & 2) ? 5 : 1) void xfg_classify_kernel(const xfg_kargs a)
+// ---------------------------------------------------------------- counters and stats
+// Per-workgroup counter state.  A hit adds 1 << COUNTER_SHIFT to the first
+// matching rule's value (xdp-filter/xdpfilt_prog.h:60-61), i.e. 1 to its
+// `hits` word.  Per-CPU values made that a plain add in the reference; here
+// many waves add to one table, so a bump goes, in order of preference, to
+//   * a direct LDS counter (rule sets of at most XFG_DCNT_MAX counters),
+//   * the LDS counter cache (lanes of a wave on the same rule are merged
+//     first; a hot rule, e.g. a ruled port, is summed here and reaches
+//     memory once per workgroup),
+//   * a memory-side atomic.
+// The pipelined kernels send their hash-map hits to the hit log instead
+// (HitLog below): random memory-side atomics are what bounds a 1M-rule
+// table's millions of cold hits per launch.
+struct Counters {
+	uint32_t *ctag, *ccnt;   // LDS counter cache, CC_ENTRIES each
+	uint32_t *dcnt;          // LDS direct counters, a.dcnt of them
+
+	__device__ __forceinline__ void init(const xfg_kargs &a, int tid, int nthr)
+	{
+		for (int i = tid; i < CC_ENTRIES; i += nthr) {
+			ctag[i] = CT_NONE;
+			ccnt[i] = 0;
+		}
+		for (uint32_t i = tid; i < a.dcnt; i += nthr)
+			dcnt[i] = 0;
+	}
+	// Bump the counter of every lane's tag (CT_NONE: none).  Whole wave.
+	__device__ __forceinline__ void bump(const xfg_kargs &a, uint32_t tag, int lane)
+	{
+		const unsigned long long pend = __ballot(tag != CT_NONE);
+		if (!pend)
+			return;
+		const int leader = __ffsll((long long)pend) - 1;
+		const uint32_t lt = __shfl(tag, leader);
+		const bool mine = tag == lt;
+		const unsigned long long same = __ballot(mine);
+		if (lane == leader) {
+			const uint32_t cnt = (uint32_t)__popcll(same);
+			if (lt < a.dcnt)
+				atomicAdd(&dcnt[lt], cnt);
+			else if (!cache_hit(ctag, ccnt, lt, cnt))
+				atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
+		}
+		if (mine)
+			tag = CT_NONE;
+		if (tag != CT_NONE) {
+			if (tag < a.dcnt)
+				atomicAdd(&dcnt[tag], 1u);
+			else if (!cache_hit(ctag, ccnt, tag, 1))
+				atomicAdd(global_counter(a, tag), 1ull);
+		}
+	}
+	// Workgroup end (after a barrier): LDS sums to memory.
+	__device__ __forceinline__ void flush(const xfg_kargs &a, int tid, int nthr)
+	{
+		for (int i = tid; i < CC_ENTRIES; i += nthr)
+			if (ctag[i] != CT_NONE && ccnt[i])
+				atomicAdd(global_counter(a, ctag[i]), (unsigned long long)ccnt[i]);
+		for (uint32_t i = tid; i < a.dcnt; i += nthr)
+			if (dcnt[i])
+				atomicAdd(global_counter(a, i), (unsigned long long)dcnt[i]);
+	}
+};
+
+// ---------------------------------------------------------------- hit log
+// The pipelined kernels' counting of hash-map hits (kargs.tlog != NULL):
+//   1. each wave appends its hits' counter identities to its own region,
+//      one coalesced store per tile (log_append);
+//   2. at its end each workgroup sorts its entries by partition
+//      (g >> 4) % XFG_LOG_PARTS -- 16 consecutive counters, one 128-byte
+//      line of u64, per chunk; chunks dealt round-robin -- reserving its
+//      slice of every partition's buffer with one atomic per partition
+//      (log_partition);
+//   3. xfg_log_count_kernel, one workgroup per partition, sums the
+//      partition in an LDS histogram and adds each count to its counter
+//      with a plain read-modify-write (it owns those counters).
+// Every hit costs a 4-byte coalesced store and two L2-resident passes
+// instead of a random memory-side atomic.  A partition buffer that would
+// overflow sends the excess to atomics (exact either way).
+__device__ __forceinline__ uint32_t log_part(uint32_t g) { return (g >> 4) & (XFG_LOG_PARTS - 1); }
+__device__ __forceinline__ uint32_t log_local(uint32_t g) { return ((g >> 12) << 4) | (g & 15); }
+
+__device__ __forceinline__ void log_append(uint32_t *region, uint32_t &cnt, uint32_t tag, int lane)
 {
-	constexpr int CPP = W / 16;            // 16-byte chunks per packet window
-	constexpr int ROWDW = Pkt<W>::ROWDW;   // odd dword stride per LDS row
+	const unsigned long long m = __ballot(tag != CT_NONE);
+	if (m) {
+		if (tag != CT_NONE)
+			region[cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = tag;
+		cnt += (uint32_t)__popcll(m);
+	}
+}
+
+// Workgroup end: the NW wave regions (counts in s_n) into the partition
+// buffers.  s_h, s_b: LDS scratch of XFG_LOG_PARTS words each.  Whole
+// workgroup, after a barrier.
+template <int NW>
+__device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t *s_n, uint32_t *s_h,
+					      uint32_t *s_b, int tid, int nthr)
+{
+	const uint64_t r0 = (uint64_t)blockIdx.x * NW * a.defer_cap;
+	for (int i = tid; i < (int)XFG_LOG_PARTS; i += nthr)
+		s_h[i] = 0;
+	__syncthreads();
+	for (int w = 0; w < NW; w++) {
+		const uint32_t *reg = a.tlog + r0 + (uint64_t)w * a.defer_cap;
+		for (uint32_t e = tid; e < s_n[w]; e += nthr)
+			atomicAdd(&s_h[log_part(reg[e])], 1u);
+	}
+	__syncthreads();
+	for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
+		const uint32_t c = s_h[p];
+		s_b[p] = c ? atomicAdd(&a.pfill[p], c) : 0;
+		s_h[p] = 0;   // now the cursor
+	}
+	__syncthreads();
+	for (int w = 0; w < NW; w++) {
+		const uint32_t *reg = a.tlog + r0 + (uint64_t)w * a.defer_cap;
+		for (uint32_t e = tid; e < s_n[w]; e += nthr) {
+			const uint32_t g = reg[e], p = log_part(g);
+			const uint32_t pos = s_b[p] + atomicAdd(&s_h[p], 1u);
+			if (pos < a.pcap)
+				a.pbuf[(uint64_t)p * a.pcap + pos] = g;
+			else
+				atomicAdd(global_counter(a, g), 1ull);
+		}
+	}
+}
+
+// Per-action {packets, bytes} (xdp_stats_record_action,
+// headers/xdp/xdp_stats_kern.h:29-48), summed per lane, then per wave, per
+// workgroup (LDS) and once per workgroup into the device's stats.
+struct LaneStats {
+	uint32_t c0 = 0, c1 = 0, c2 = 0;
+	unsigned long long b0 = 0, b1 = 0, b2 = 0;
+	// (selects, not a branch on act: an indexed update would go to scratch)
+	__device__ __forceinline__ void add(uint32_t act, uint32_t len)
+	{
+		c0 += act == A_ABORTED;
+		c1 += act == A_DROP;
+		c2 += act == A_PASS;
+		b0 += act == A_ABORTED ? len : 0u;
+		b1 += act == A_DROP ? len : 0u;
+		b2 += act == A_PASS ? len : 0u;
+	}
+	// to s_stats[6] (LDS, zeroed before), by every wave
+	__device__ __forceinline__ void reduce(unsigned long long *s_stats, int lane) const
+	{
+		unsigned long long v[6] = { c0, b0, c1, b1, c2, b2 };
+#pragma unroll
+		for (int k = 0; k < 6; k++) {
+			unsigned long long x = v[k];
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1)
+				x += __shfl_xor(x, o);
+			if (lane == 0 && x)
+				atomicAdd(&s_stats[k], x);
+		}
+	}
+};
+
+// The whole reference program for one packet read from HBM (no staged
+// window): the general path's and the deferred packets' classification.
+template <uint32_t FEAT>
+__device__ __forceinline__ uint32_t classify_one(const xfg_kargs &a, const uint32_t *s_ports,
+					      uint64_t gi, uint32_t len, uint32_t &tag)
+{
+	Pkt<0> p{ nullptr, pkt_ptr(a, gi), len };
+	const Parsed r = parse<FEAT, 0>(p);
+	return lookups<FEAT, false>(a, LazyKeys<Pkt<0>>{ p }, r, s_ports, tag);
+}
+
+// Stage the ruled ports into LDS: the table into s_tab (static), or the
+// nibble map into s_nib (the front of the dynamic LDS); returns the one the
+// lookups read.
+template <uint32_t FEAT>
+__device__ __forceinline__ const uint32_t *stage_ports(const xfg_kargs &a, uint32_t *s_tab,
+						       uint32_t *s_nib, int tid, int nthr)
+{
+	if constexpr ((FEAT & (F_UDP | F_TCP)) != 0) {
+		if (a.port_count && a.port_tab) {
+			for (int i = tid; i < (int)XFG_PORT_TAB; i += nthr)
+				s_tab[i] = a.port_tab[i];
+		} else if (a.port_count) {
+			for (int i = tid; i < (int)XFG_PORT_NIB_WORDS; i += nthr)
+				s_nib[i] = a.port_nib[i];
+			return s_nib;
+		}
+	}
+	return s_tab;
+}
+
+// Dynamic LDS of a classify kernel: the port nibble map (when used), then
+// the direct counters.
+__device__ __forceinline__ uint32_t *dcnt_base(const xfg_kargs &a, uint32_t *s_dyn)
+{
+	return s_dyn + (a.port_nib && !a.port_tab && a.port_count ? XFG_PORT_NIB_WORDS : 0);
+}
+
+// ---------------------------------------------------------------- general kernel
+// Every batch layout (offsets, AF_XDP descriptors, strides below the window,
+// lengths that must bound the window loads).  A workgroup of 256 lanes walks
+// tiles of 256 packets (one per lane): the next tile's windows are loaded
+// into registers while the current one is processed, staged into LDS rows
+// of W + 4 bytes (odd dword stride: conflict-free lane-per-packet reads),
+// parsed (xdpfilt_prog.h:224-307 over headers/xdp/parsing_helpers.h) and
+// looked up in reference order (`lookups`).
+template <uint32_t FEAT, int W>
+__global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
+{
+	constexpr int CPP = W / 16;
+	constexpr int ROWDW = Pkt<W>::ROWDW;
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	__shared__ uint32_t win[TILE * ROWDW];
-	__shared__ uint32_t s_pbits[PORTS ? 2048 : 1];
+	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
 	__shared__ unsigned long long s_stats[6];
-	extern __shared__ uint32_t s_pcnt[];   // hit-log fill per partition (hlog_parts)
+	extern __shared__ uint32_t s_dyn[];
 
-	const int tid = threadIdx.x;
-	const int lane = tid & 63;
+	const int tid = threadIdx.x, lane = tid & 63;
+	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
+	cn.init(a, tid, TILE);
 	if (tid < 6)
 		s_stats[tid] = 0;
-	for (int i = tid; i < CC_ENTRIES; i += TILE) {
-		s_ctag[i] = CT_NONE;
-		s_ccnt[i] = 0;
-	}
-	if (a.hlog)
-		for (uint32_t i = tid; i < a.hlog_parts; i += TILE)
-			s_pcnt[i] = 0;
-	for (uint32_t i = tid; i < a.dcnt; i += TILE)   // (s_pcnt holds the direct counters)
-		s_pcnt[i] = 0;
-	if constexpr (PORTS) {
-		if (a.port_count)
-			for (int i = tid; i < 2048; i += TILE)
-				s_pbits[i] = a.port_tab ? a.port_tab[i] : a.port_bits[i];
-	}
-	// fixed-stride layout with stride >= W: every window byte is readable,
-	// so loads need no length (no load->load dependency on the stream)
-	const bool guarded = a.offsets != nullptr || a.stride < (uint32_t)W;
+	const uint32_t *s_ports = stage_ports<FEAT>(a, s_tab, s_dyn, tid, TILE);
+	__syncthreads();
 
-	// WT (V & 8): every wave walks its own tiles of 64 packets with its own
-	// LDS rows, so no workgroup barrier sits in the loop; otherwise tiles of
-	// TILE packets shared by the workgroup's four waves.
-	constexpr bool WT = (V & 8) != 0;
-	constexpr int U = WT ? 64 : TILE;          // packets per tile
-	const int me = WT ? lane : tid;            // this lane's packet within the tile
-	uint32_t *const wrows = WT ? win + (tid >> 6) * 64 * ROWDW : win;
-	const uint64_t ntiles = (a.n + U - 1) / U;
-	const uint64_t tstep = WT ? (uint64_t)gridDim.x * (TILE / 64) : gridDim.x;
-	// dense layout (stride == W, no offsets): a tile is one contiguous block
-	// of U * W bytes and chunk c of it sits at byte 16 * c
-	const bool dense = !guarded && a.stride == (uint32_t)W;
-	uint64_t tile = WT ? (uint64_t)blockIdx.x * (TILE / 64) + (tid >> 6) : blockIdx.x;
+	const uint64_t ntiles = (a.n + TILE - 1) / TILE;
+	uint64_t tile = blockIdx.x;
 	u32x4 pre[CPP];
 	uint32_t plen = 0;
-	uint32_t c_ab = 0, c_dr = 0, c_pa = 0;
-	unsigned long long b_ab = 0, b_dr = 0, b_pa = 0;
+	LaneStats st;
 	auto issue = [&](uint64_t t) {
-		const uint64_t base = t * U;
-		if constexpr (DENSE) {
-			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + base * W) + me;
-			const uint32_t rem = a.n - base >= (uint64_t)U ? U : (uint32_t)(a.n - base);
-#pragma unroll
-			for (int it = 0; it < CPP; it++) {
-				pre[it] = u32x4{ 0, 0, 0, 0 };
-				if ((uint32_t)(it * U + me) / CPP < rem)
-					pre[it] = __builtin_nontemporal_load(src + it * U);
-			}
-			plen = base + me < a.n ? load_len(a, base + me) : 0;
-			return;
-		}
-		if (dense && base + U <= a.n) {
-			const u32x4 *src = reinterpret_cast<const u32x4 *>(a.data + base * W) + me;
-#pragma unroll
-			for (int it = 0; it < CPP; it++)
-				pre[it] = __builtin_nontemporal_load(src + it * U);
-		} else {
-#pragma unroll
-			for (int it = 0; it < CPP; it++) {
-				const int c = it * U + me;
-				const int pk = c / CPP, sub = c % CPP;
-				const uint64_t gi = base + pk;
-				pre[it] = u32x4{ 0, 0, 0, 0 };
-				if (gi < a.n && (!guarded || (uint32_t)sub * 16 < load_len(a, gi)))
-					pre[it] = __builtin_nontemporal_load(
-						reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16));
-			}
-		}
-		plen = base + me < a.n ? load_len(a, base + me) : 0;
-	};
-	auto tile_sync = [&]() {
-		if constexpr (WT)
-			__builtin_amdgcn_wave_barrier();   // rows are this wave's own
-		else
-			__syncthreads();
-	};
-#ifndef XFG_EXP_NO_PREFETCH
-	if (tile < ntiles)
-		issue(tile);
-#endif
-	constexpr bool PROF = (V & 4) != 0;
-	__shared__ uint32_t s_prof[PROF ? NPHASE : 1];
-	Stamps st;
-	if constexpr (PROF)
-		st.init(s_prof);
-
-	for (; tile < ntiles; tile += tstep) {
-		const uint64_t base = tile * U;
-#ifdef XFG_EXP_NO_PREFETCH
-		issue(tile);
-#endif
-		if constexpr (PROF)
-			st.mark(7);   // end-of-tile bookkeeping + loop
-		// 1. stage the prefetched windows into LDS
+		const uint64_t base = t * TILE;
 #pragma unroll
 		for (int it = 0; it < CPP; it++) {
-			const int c = it * U + me;
+			const int c = it * TILE + tid;
 			const int pk = c / CPP, sub = c % CPP;
-			uint32_t *dst = &wrows[pk * ROWDW + sub * 4];
+			const uint64_t gi = base + pk;
+			pre[it] = u32x4{ 0, 0, 0, 0 };
+			if (gi < a.n && (uint32_t)sub * 16 < load_len(a, gi))
+				pre[it] = __builtin_nontemporal_load(
+					reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16));
+		}
+		plen = base + tid < a.n ? load_len(a, base + tid) : 0;
+	};
+	if (tile < ntiles)
+		issue(tile);
+	for (; tile < ntiles; tile += gridDim.x) {
+		const uint64_t base = tile * TILE;
+#pragma unroll
+		for (int it = 0; it < CPP; it++) {
+			const int c = it * TILE + tid;
+			const int pk = c / CPP, sub = c % CPP;
+			uint32_t *dst = &win[pk * ROWDW + sub * 4];
 			dst[0] = pre[it].x;
 			dst[1] = pre[it].y;
 			dst[2] = pre[it].z;
 			dst[3] = pre[it].w;
 		}
 		const uint32_t len = plen;
-		if constexpr (PROF) {
-			asm volatile("" ::"v"(len));
-			st.mark(0);   // prefetched windows landed and written to LDS
-		}
-		tile_sync();
-		if constexpr (PROF)
-			st.mark(1);   // barrier
-#ifndef XFG_EXP_NO_PREFETCH
-		if (tile + tstep < ntiles)
-			issue(tile + tstep);   // next tile's stream overlaps this tile's work
-#endif
-		if constexpr (PROF)
-			st.mark(2);   // next tile issued
-
-		// 2-4. parse, match, verdict
-		const uint64_t gi = base + me;
-		uint32_t act = A_NONE;
-		uint32_t tag = CT_NONE;
+		__syncthreads();
+		if (tile + gridDim.x < ntiles)
+			issue(tile + gridDim.x);   // next tile's stream overlaps this tile's work
+		const uint64_t gi = base + tid;
+		uint32_t act = A_NONE, tag = CT_NONE;
 		if (gi < a.n) {
-			Pkt<W> p{ &wrows[me * ROWDW], pkt_ptr(a, gi), len };
-			if (a.ablate & 4) {
-				act = p.u8(0) & 1;
-			} else {
-				const Parsed r = parse<FEAT, W>(p);
-				if constexpr (PROF) {
-					asm volatile("" ::"v"(r.abort_at), "v"(r.k4a), "v"(r.l3));
-					st.mark(3);   // parse
-				}
-				act = lookups<FEAT, (V & 1) != 0>(a, LazyKeys<Pkt<W>>{ p }, r, s_pbits, tag);
-			}
-			if constexpr (PROF) {
-				asm volatile("" ::"v"(act), "v"(tag));
-				st.mark(4);   // lookups
-			}
+			Pkt<W> p{ &win[tid * ROWDW], pkt_ptr(a, gi), len };
+			const Parsed r = parse<FEAT, W>(p);
+			act = lookups<FEAT, false>(a, LazyKeys<Pkt<W>>{ p }, r, s_ports, tag);
 			a.verdicts[gi] = (uint8_t)act;
 		}
-		if (a.ablate & 2)
-			tag = CT_NONE;
-		if constexpr ((FEAT & X_NOCNT) != 0)
-			tag = CT_NONE;
-
-		// counter bump: lanes of the wave hitting the same rule are merged
-		// (one leader round), then summed in the LDS counter cache; a bump
-		// the cache cannot take goes straight to a memory-side atomic
-		{
-			const unsigned long long pend = __ballot(tag != CT_NONE);
-			if (pend) {
-				const int leader = __ffsll((long long)pend) - 1;
-				const uint32_t lt = __shfl(tag, leader);
-				const bool mine = tag == lt;
-				const unsigned long long same = __ballot(mine);
-				if (lane == leader) {
-					const uint32_t cnt = (uint32_t)__popcll(same);
-					if (lt < a.dcnt)
-						atomicAdd(&s_pcnt[lt], cnt);
-					else if (!cache_hit(s_ctag, s_ccnt, lt, cnt)) {
-						if (cnt > 1)
-							atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
-						else
-							cold_bump(a, s_pcnt, lt);
-					}
-				}
-				if (mine)
-					tag = CT_NONE;
-			}
-		}
-		if (tag != CT_NONE && tag < a.dcnt)
-			atomicAdd(&s_pcnt[tag], 1u);
-		else if (tag != CT_NONE && !cache_hit(s_ctag, s_ccnt, tag, 1))
-			cold_bump(a, s_pcnt, tag);
-
-		// 5. per-action stats (xdp_stats_record_action), kept per lane
-#ifdef XFG_EXP_NO_STATS
-		if (0) {
-#else
-		if (act == A_ABORTED) {
-#endif
-			c_ab++;
-			b_ab += len;
-		} else if (act == A_DROP) {
-			c_dr++;
-			b_dr += len;
-		} else if (act == A_PASS) {
-			c_pa++;
-			b_pa += len;
-		}
-		if constexpr (PROF)
-			st.mark(5);   // counters, verdict, stats
-		tile_sync();   // LDS window reuse
-		if constexpr (PROF)
-			st.mark(6);   // end barrier
+		cn.bump(a, tag, lane);
+		st.add(act, len);
+		__syncthreads();   // LDS window reuse
 	}
-	if constexpr (PROF)
-		st.store(a.prof);
-	// per-action stats: lane sums -> wave sums -> workgroup (LDS) -> device
-	{
-		unsigned long long v[6] = { c_ab, b_ab, c_dr, b_dr, c_pa, b_pa };
-#pragma unroll
-		for (int k = 0; k < 6; k++) {
-			unsigned long long x = v[k];
-#pragma unroll
-			for (int o = 32; o > 0; o >>= 1)
-				x += __shfl_xor(x, o);
-			if (lane == 0 && x)
-				atomicAdd(&s_stats[k], x);
-		}
-	}
+	st.reduce(s_stats, lane);
 	__syncthreads();
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
-	for (int i = tid; i < CC_ENTRIES; i += TILE)
-		if (s_ctag[i] != CT_NONE && s_ccnt[i])
-			atomicAdd(global_counter(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
-	if (a.hlog)
-		for (uint32_t p = tid; p < a.hlog_parts; p += TILE)
-			a.hlog_cnt[(uint64_t)p * gridDim.x + blockIdx.x] =
-				s_pcnt[p] < a.hlog_cap ? s_pcnt[p] : a.hlog_cap;
-	for (uint32_t i = tid; i < a.dcnt; i += TILE)
-		if (s_pcnt[i])
-			atomicAdd(global_counter(a, i), (unsigned long long)s_pcnt[i]);
+	cn.flush(a, tid, TILE);
 }
 
-// ---------------------------------------------------------------- streamed kernel
-// The fixed-stride layout (stride >= 64, 16-byte aligned) with the header
-// stream taken off the lookup waves.  A workgroup is four lookup waves (one
-// packet per lane) plus one I/O wave:
-//
-//   I/O wave      global_load_lds (LDS-DMA, no VGPRs) of tile k+2's header
-//                 windows and lengths into the buffer tile k has just
-//                 released; then the counter atomics and the verdict store
-//                 of tile k-1, read from LDS;
-//   lookup waves  parse tile k from LDS, copy its keys to registers, release
-//                 the buffer (barrier P), probe, and leave verdict bytes and
-//                 cold counter bumps in LDS (barrier E).
-//
-// A wave's vector-memory counter completes in issue order, so a lookup wave
-// that also streamed headers or issued atomics would wait for them at every
-// probe; here its counter holds nothing but its own probes.
-//
-// Tile buffer: 256 windows of 64 bytes, 16-byte chunk c of packet p at chunk
-// slot p*4 + (c ^ ((p >> 2) & 3)): every LDS-DMA instruction writes 1 KiB
-// lane-linearly (the swizzle is applied to the source address), and a lane-
-// per-packet read of any dword touches 16 distinct banks per 16 lanes.
-constexpr int IO_THREADS = TILE + 64;
-constexpr int SBUF_DW = TILE * 16;   // one tile buffer, dwords
+#include "xfg_pipeline.hip"
 
-__device__ __forceinline__ uint32_t lds_addr(const void *p)
+// ---------------------------------------------------------------- hit-log count
+// One workgroup per log partition (see HitLog): sums the partition's buffer
+// in an LDS histogram, then adds each non-zero count to its counter with a
+// plain read-modify-write (the workgroup owns the partition's counters),
+// and resets the partition's fill for the next launch.
+constexpr int LC_THREADS = 512;
+
+__global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kargs a, uint32_t hist_n)
 {
-	return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
-
-// 16 bytes per lane from gsrc to LDS lds + 16 * lane (lds wave-uniform).  The
-// compiler does not see this load: its completion is counted by hand.
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds)
-{
-	unsigned keep;
-	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-		     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-		     : "=&s"(keep)
-		     : "v"(gsrc), "s"(lds)
-		     : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm()
-{
-	asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-// Wait until at most y (wave-uniform, <= 23) vector-memory operations of this
-// wave are outstanding.
-__device__ __forceinline__ void wait_vm_dyn(uint32_t y)
-{
-	switch (y) {
-#define XFG_W(n) case n: wait_vm<n>(); break;
-	XFG_W(1) XFG_W(2) XFG_W(3) XFG_W(4) XFG_W(5) XFG_W(6) XFG_W(7) XFG_W(8)
-	XFG_W(9) XFG_W(10) XFG_W(11) XFG_W(12) XFG_W(13) XFG_W(14) XFG_W(15) XFG_W(16)
-	XFG_W(17) XFG_W(18) XFG_W(19) XFG_W(20) XFG_W(21) XFG_W(22) XFG_W(23)
-#undef XFG_W
-	default: wait_vm<0>(); break;
-	}
-}
-
-// Workgroup barrier that waits for this wave's LDS operations only (an LDS-
-// DMA in flight stays in flight; __syncthreads() would drain it).
-__device__ __forceinline__ void wg_barrier()
-{
-	asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// Packet view over a swizzled tile buffer (same interface as Pkt<64>).
-struct SPkt {
-	const uint32_t *tb;   // tile buffer
-	uint32_t base;        // 16 * p
-	uint32_t xr;          // (p >> 2) & 3
-	const uint8_t *g;
-	uint32_t len;
-
-	__device__ __forceinline__ uint32_t dw(uint32_t k) const
-	{
-		return tb[base + (((k >> 2) ^ xr) << 2) + (k & 3)];
-	}
-	__device__ __forceinline__ uint32_t u8(uint32_t o) const
-	{
-		if (o < 64)
-			return (dw(o >> 2) >> (8 * (o & 3))) & 0xff;
-		return gbyte(g, o);
-	}
-	__device__ __forceinline__ uint32_t u32(uint32_t o) const
-	{
-		if (o + 4 <= 64) {
-			const uint32_t k = o >> 2;
-			return __builtin_amdgcn_alignbyte(dw(k < 15 ? k + 1 : 15), dw(k), o & 3);
-		}
-		return gbyte(g, o) | (gbyte(g, o + 1) << 8) | (gbyte(g, o + 2) << 16) |
-		       (gbyte(g, o + 3) << 24);
-	}
-	__device__ __forceinline__ uint32_t raw16(uint32_t o) const
-	{
-		if (o + 2 <= 64) {
-			const uint32_t k = o >> 2;
-			return __builtin_amdgcn_alignbyte(dw(k < 15 ? k + 1 : 15), dw(k), o & 3) & 0xffffu;
-		}
-		return gbyte(g, o) | (gbyte(g, o + 1) << 8);
-	}
-	__device__ __forceinline__ uint32_t be16(uint32_t o) const
-	{
-		uint32_t r = raw16(o);
-		return ((r & 0xff) << 8) | (r >> 8);
-	}
-};
-
-// Lookup keys copied to registers before the tile buffer is released; the
-// NDISC target (rare) is read from the packet in HBM.
-struct RegKeys {
-	uint32_t e0, e1, e2;          // bytes 0..11: dst MAC, src MAC
-	uint32_t d6[4], s6[4];        // IPv6 daddr, saddr
-	const uint8_t *g;
-
-	__device__ __forceinline__ void eth(uint32_t o, uint32_t &lo, uint32_t &hi) const
-	{
-		if (o == 0) {
-			lo = e0;
-			hi = e1 & 0xffff;
-		} else {
-			lo = __builtin_amdgcn_alignbyte(e2, e1, 2);
-			hi = e2 >> 16;
-		}
-	}
-	__device__ __forceinline__ void v6_dst(uint32_t, uint32_t (&k)[4]) const
-	{
-		k[0] = d6[0]; k[1] = d6[1]; k[2] = d6[2]; k[3] = d6[3];
-	}
-	__device__ __forceinline__ void v6_src(uint32_t, uint32_t (&k)[4]) const
-	{
-		k[0] = s6[0]; k[1] = s6[1]; k[2] = s6[2]; k[3] = s6[3];
-	}
-	__device__ __forceinline__ void nd_tgt(uint32_t o, uint32_t (&k)[4]) const
-	{
-#pragma unroll
-		for (int i = 0; i < 4; i++) {
-			const uint8_t *q = g + o + 4 * i;
-			k[i] = gbyte(q, 0) | (gbyte(q, 1) << 8) | (gbyte(q, 2) << 16) | (gbyte(q, 3) << 24);
-		}
-	}
-};
-
-template <uint32_t FEAT, int V>
-__global__ __launch_bounds__(IO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void xfg_classify_stream_kernel(const xfg_kargs a)
-{
-	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
-	__shared__ __attribute__((aligned(16))) uint32_t ring[2 * SBUF_DW];
-	__shared__ __attribute__((aligned(16))) uint32_t s_lens[2][TILE];
-	__shared__ uint32_t s_verd[2][TILE / 4];
-	__shared__ uint32_t s_q[2][TILE];
-	__shared__ uint32_t s_qn[2];
-	__shared__ uint32_t s_pbits[PORTS ? 2048 : 1];
-	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
-	__shared__ unsigned long long s_stats[6];
-
-	const int tid = threadIdx.x;
-	const int lane = tid & 63;
-	const bool io = tid >= TILE;
-	if (tid < 6)
-		s_stats[tid] = 0;
-	if (tid < 2)
-		s_qn[tid] = 0;
-	for (int i = tid; i < CC_ENTRIES; i += IO_THREADS) {
-		s_ctag[i] = CT_NONE;
-		s_ccnt[i] = 0;
-	}
-	if constexpr (PORTS) {
-		if (a.port_count)
-			for (int i = tid; i < 2048; i += IO_THREADS)
-				s_pbits[i] = a.port_tab ? a.port_tab[i] : a.port_bits[i];
-	}
-
-	const uint64_t ntiles = (a.n + TILE - 1) / TILE;
-	const uint64_t G = gridDim.x;
-	const uint64_t b = blockIdx.x;
-	const uint64_t K = b < ntiles ? (ntiles - 1 - b) / G + 1 : 0;
-	const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
-	const uint32_t lens_lds = __builtin_amdgcn_readfirstlane(lds_addr(&s_lens[0][0]));
-	const uint32_t esz = a.lens_u16 ? 2 : 4;
-
-	// I/O wave: 17 LDS-DMA instructions per tile (16 window KiBs + lengths).
-	// Instruction j, lane l loads packet 16j + l/4, chunk c(l) = (l & 3) ^
-	// ((l >> 4) & 3) (the swizzle; independent of j), so a lane's source
-	// address advances by 16 packets per instruction.
-	const uint64_t io_off = (uint64_t)(lane >> 2) * a.stride + 16u * ((lane & 3) ^ ((lane >> 4) & 3));
-	auto io_issue = [&](uint64_t k) {
-		const uint64_t p0 = (b + k * G) * TILE;
-		const uint32_t ldsb = ring_lds + (uint32_t)(k & 1) * (SBUF_DW * 4);
-		const uint64_t step = 16ull * a.stride;
-		const uint8_t *src = a.data + p0 * a.stride + io_off;
-		if (p0 + TILE <= a.n) {
-#pragma unroll
-			for (int j = 0; j < 16; j++) {
-				glds16(src, __builtin_amdgcn_readfirstlane(ldsb + j * 1024));
-				src += step;
-			}
-		} else {
-#pragma unroll
-			for (int j = 0; j < 16; j++) {
-				const uint64_t gi = p0 + 16 * j + (lane >> 2);
-				glds16(gi < a.n ? src : a.data, __builtin_amdgcn_readfirstlane(ldsb + j * 1024));
-				src += step;
-			}
-		}
-		const uint64_t first = p0 + (uint64_t)lane * (16 / esz);
-		const uint8_t *lsrc = static_cast<const uint8_t *>(a.lens);
-		if (lane < (a.lens_u16 ? 32 : 64))
-			glds16(first < a.n ? lsrc + first * esz : lsrc,
-			       __builtin_amdgcn_readfirstlane(lens_lds + (uint32_t)(k & 1) * (TILE * 4)));
-	};
-	// I/O wave: counter atomics and verdict bytes of tile k (LDS parity
-	// k & 1).  Returns a lower bound of the vector-memory instructions it
-	// issued (exact on full tiles): one per 64 queued bumps, one store.
-	auto io_flush = [&](uint64_t k) -> uint32_t {
-		const uint32_t q = (uint32_t)(k & 1);
-		const uint32_t nq = (a.ablate & 2) ? 0 : s_qn[q];
-		uint32_t ops = 0;
-#pragma unroll
-		for (uint32_t i = 0; i < TILE / 64; i++) {
-			if (i * 64 < nq) {   // wave-uniform: lane 0 is active below
-				ops++;
-				if (i * 64 + lane < nq)
-					atomicAdd(global_counter(a, s_q[q][i * 64 + lane]), 1ull);
-			}
-		}
-		const uint64_t p0 = (b + k * G) * TILE;
-		const uint32_t v = s_verd[q][lane];
-		if (p0 + TILE <= a.n && !((uintptr_t)a.verdicts & 3)) {
-			reinterpret_cast<uint32_t *>(a.verdicts + p0)[lane] = v;
-			ops++;
-		} else {
-#pragma unroll
-			for (int i = 0; i < 4; i++)
-				if (p0 + lane * 4 + i < a.n)
-					a.verdicts[p0 + lane * 4 + i] = (uint8_t)(v >> (8 * i));
-		}
-		if (lane == 0)
-			s_qn[q] = 0;
-		return ops;
-	};
-
-	uint32_t c_ab = 0, c_dr = 0, c_pa = 0;
-	unsigned long long b_ab = 0, b_dr = 0, b_pa = 0;
-
-	if (io) {
-		if (K > 0)
-			io_issue(0);
-		if (K > 1) {
-			io_issue(1);
-			wait_vm<17>();
-		} else {
-			wait_vm<0>();
-		}
-	}
-	wg_barrier();   // S: LDS set up, tile 0 landed
-
-	for (uint64_t k = 0; k < K; k++) {
-		const uint32_t par = (uint32_t)(k & 1);
-		if (io) {
-			wg_barrier();   // P_k: tile k parsed, its buffer free
-			// issue order F(k-1), I(k+2): wait for I(k+1) (issued a step
-			// ago, older than both) and whatever preceded it
-			uint32_t younger = k >= 1 ? io_flush(k - 1) : 0;
-			if (k + 2 < K) {
-				io_issue(k + 2);
-				younger += 17;
-			}
-			if (k + 1 < K)
-				wait_vm_dyn(younger);
-			wg_barrier();   // E_k
-			continue;
-		}
-		// lookup waves
-		const uint64_t gi = (b + k * G) * TILE + tid;
-		const bool valid = gi < a.n;
-		const uint32_t len = a.lens_u16 ? reinterpret_cast<const uint16_t *>(s_lens[par])[tid]
-						: s_lens[par][tid];
-		const SPkt p{ ring + par * SBUF_DW, (uint32_t)tid * 16, ((uint32_t)tid >> 2) & 3,
-			      a.data + gi * a.stride, len };
-		Parsed r;
-		RegKeys ks;
-		ks.g = p.g;
-		uint32_t act = A_NONE;
-		if (valid) {
-			if (a.ablate & 4) {
-				act = p.u8(0) & 1;
-			} else {
-				r = parse<FEAT, 64>(p);
-				if constexpr ((FEAT & F_ETH) != 0) {
-					ks.e0 = p.dw(0);
-					ks.e1 = p.dw(1);
-					ks.e2 = p.dw(2);
-				}
-				if constexpr ((FEAT & F_IPV6) != 0) {
-					if (r.l3 == 3) {
-#pragma unroll
-						for (int i = 0; i < 4; i++) {
-							ks.s6[i] = p.u32(r.o6 + 8 + 4 * i);
-							ks.d6[i] = p.u32(r.o6 + 24 + 4 * i);
-						}
-					}
-				}
-			}
-		}
-		wg_barrier();   // P_k
-		uint32_t tag = CT_NONE;
-		if (valid && !(a.ablate & 4))
-			act = lookups<FEAT, (V & 1) != 0>(a, ks, r, s_pbits, tag);
-		reinterpret_cast<uint8_t *>(s_verd[par])[tid] = (uint8_t)act;
-		if (a.ablate & 2)
-			tag = CT_NONE;
-
-		// counter bump: wave leader merge, LDS counter cache, else queue the
-		// bump for the I/O wave
-		bool cold = false;
-		{
-			const unsigned long long pend = __ballot(tag != CT_NONE);
-			if (pend) {
-				const int leader = __ffsll((long long)pend) - 1;
-				const uint32_t lt = __shfl(tag, leader);
-				const bool mine = tag == lt;
-				const unsigned long long same = __ballot(mine);
-				const uint32_t cnt = (uint32_t)__popcll(same);
-				if (lane == leader && !cache_hit(s_ctag, s_ccnt, lt, cnt)) {
-					if (cnt == 1)
-						cold = true;
-					else
-						atomicAdd(global_counter(a, lt), (unsigned long long)cnt);
-				}
-				if (mine && !cold)
-					tag = CT_NONE;
-			}
-		}
-		if (tag != CT_NONE && !cold) {
-			if (cache_hit(s_ctag, s_ccnt, tag, 1))
-				tag = CT_NONE;
-			else
-				cold = true;
-		}
-		{
-			const unsigned long long m = __ballot(cold);
-			if (m) {
-				const int first = __ffsll((long long)m) - 1;
-				uint32_t qb = 0;
-				if (lane == first)
-					qb = atomicAdd(&s_qn[par], (uint32_t)__popcll(m));
-				qb = __shfl(qb, first);
-				if (cold) {
-					const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-						(uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-					s_q[par][qb + rank] = tag;
-				}
-			}
-		}
-
-		if (act == A_ABORTED) {
-			c_ab++;
-			b_ab += len;
-		} else if (act == A_DROP) {
-			c_dr++;
-			b_dr += len;
-		} else if (act == A_PASS) {
-			c_pa++;
-			b_pa += len;
-		}
-		wg_barrier();   // E_k
-	}
-	if (io && K > 0)
-		io_flush(K - 1);
-
-	{
-		unsigned long long v[6] = { c_ab, b_ab, c_dr, b_dr, c_pa, b_pa };
-#pragma unroll
-		for (int k = 0; k < 6; k++) {
-			unsigned long long x = v[k];
-#pragma unroll
-			for (int o = 32; o > 0; o >>= 1)
-				x += __shfl_xor(x, o);
-			if (lane == 0 && x)
-				atomicAdd(&s_stats[k], x);
-		}
-	}
+	extern __shared__ uint32_t hist[];
+	const uint32_t tid = threadIdx.x, p = blockIdx.x;
+	const uint32_t fill = a.pfill[p];
+	const uint32_t np = fill < a.pcap ? fill : a.pcap;
+	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
+		hist[i] = 0;
 	__syncthreads();
-	if (tid < 6 && s_stats[tid])
-		atomicAdd(&a.stats[tid], s_stats[tid]);
-	for (int i = tid; i < CC_ENTRIES; i += IO_THREADS)
-		if (s_ctag[i] != CT_NONE && s_ccnt[i])
-			atomicAdd(global_counter(a, s_ctag[i]), (unsigned long long)s_ccnt[i]);
+	const uint32_t *e = a.pbuf + (uint64_t)p * a.pcap;
+	uint32_t i = tid;
+	for (; i + 3 * LC_THREADS < np; i += 4 * LC_THREADS) {
+		const uint32_t g0 = __builtin_nontemporal_load(e + i);
+		const uint32_t g1 = __builtin_nontemporal_load(e + i + LC_THREADS);
+		const uint32_t g2 = __builtin_nontemporal_load(e + i + 2 * LC_THREADS);
+		const uint32_t g3 = __builtin_nontemporal_load(e + i + 3 * LC_THREADS);
+		atomicAdd(&hist[log_local(g0)], 1u);
+		atomicAdd(&hist[log_local(g1)], 1u);
+		atomicAdd(&hist[log_local(g2)], 1u);
+		atomicAdd(&hist[log_local(g3)], 1u);
+	}
+	for (; i < np; i += LC_THREADS)
+		atomicAdd(&hist[log_local(__builtin_nontemporal_load(e + i))], 1u);
+	__syncthreads();
+	if (tid == 0)
+		a.pfill[p] = 0;
+	const uint32_t total = a.gbase[3] + 65536u;   // + the port counters
+	for (uint32_t k = tid; k < hist_n; k += LC_THREADS) {
+		const uint32_t g = ((k >> 4) << 12) | (p << 4) | (k & 15);
+		if (hist[k] && g < total)
+			*global_counter(a, g) += hist[k];
+	}
 }
-
-#include "xfg_pipe.hip"
-#include "xfg_spec.hip"
 
 template <uint32_t FEAT>
 hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 {
-	if constexpr ((FEAT & F_IPV4) != 0) {
-		if (a.pipe && a.spec) {
-			const size_t dl = ((a.hlog ? a.hlog_parts : 0) + a.slog_parts) * 4;
-			if (a.window <= 64) {
-				if (a.dense)
-					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 64, true>), dim3(grid), dim3(TILE), dl, s, a);
-				else
-					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 64, false>), dim3(grid), dim3(TILE), dl, s, a);
-			} else {
-				if (a.dense)
-					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 128, true>), dim3(grid), dim3(TILE), dl, s, a);
-				else
-					hipLaunchKernelGGL((xfg_classify_spec_kernel<FEAT, 128, false>), dim3(grid), dim3(TILE), dl, s, a);
-			}
-			hipError_t e = hipGetLastError();
-			if (e != hipSuccess)
-				return e;
-			if (a.hlog) {
-				hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
-				if ((e = hipGetLastError()) != hipSuccess)
-					return e;
-			}
-			if (!(a.ablate & 8))
-				hipLaunchKernelGGL(xfg_spec_resolve_kernel, dim3(a.slog_parts), dim3(SR_THREADS), 0, s, a, grid);
-			return hipGetLastError();
-		}
-	}
+	const size_t dl = (size_t)a.dcnt * 4 +
+			  (a.port_nib && !a.port_tab && a.port_count ? XFG_PORT_NIB_WORDS * 4 : 0);
 	if (a.pipe) {
-		const size_t dl = a.hlog ? a.hlog_parts * 4 : 0;   // s_pcnt
-		if (a.window <= 64) {
-			if constexpr (FEAT == (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH | F_DENY)) {
-				if (a.dense && a.variant == 0x15) {   // diagnostics: 5 waves/SIMD
-					hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 64, true, 5>), dim3(grid), dim3(TILE), dl, s, a);
-					return hipGetLastError();
-				}
-			}
-			if (a.dense)
-				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 64, true>), dim3(grid), dim3(TILE), dl, s, a);
-			else
-				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 64, false>), dim3(grid), dim3(TILE), dl, s, a);
-		} else {
-			if (a.dense)
-				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 128, true>), dim3(grid), dim3(TILE), dl, s, a);
-			else
-				hipLaunchKernelGGL((xfg_classify_pipe_kernel<FEAT, 128, false>), dim3(grid), dim3(TILE), dl, s, a);
-		}
-		const hipError_t e = hipGetLastError();
-		if (e != hipSuccess || !a.hlog)
-			return e;
-		hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
-		return hipGetLastError();
-	}
-	const size_t dl = a.hlog ? a.hlog_parts * 4 : a.dcnt * 4;   // classic kernel's s_pcnt
-	if (a.streamed) {
-		hipLaunchKernelGGL((xfg_classify_stream_kernel<FEAT, 0>), dim3(grid), dim3(IO_THREADS), 0, s, a);
-		return hipGetLastError();
-	} else if (a.window <= 64) {
-		// build variants of the headline program (diagnostics: XFG_VARIANT)
-		if constexpr (FEAT == (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH | F_DENY)) {
-			switch (a.variant) {
-			case 1:
-				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 1>), dim3(grid), dim3(TILE), 0, s, a);
-				return hipGetLastError();
-			case 2:
-				if (a.dense)
-					hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 2, true>), dim3(grid), dim3(TILE), 0, s, a);
+		bool done = false;
+		if constexpr ((FEAT & F_IPV4) != 0) {
+			// key mode 1 (only IPv4 keys live): the branch-free kernel
+			if (a.km == 1) {
+				done = true;
+				if (a.window <= 64 && a.dense)
+					hipLaunchKernelGGL((xfg_pipe4_kernel<FEAT, 64, true>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
+				else if (a.window <= 64)
+					hipLaunchKernelGGL((xfg_pipe4_kernel<FEAT, 64, false>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
+				else if (a.dense)
+					hipLaunchKernelGGL((xfg_pipe4_kernel<FEAT, 128, true>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
 				else
-					hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 2>), dim3(grid), dim3(TILE), 0, s, a);
-				return hipGetLastError();
-			case 3:
-				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 3>), dim3(grid), dim3(TILE), 0, s, a);
-				return hipGetLastError();
-			case 4:
-				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 4>), dim3(grid), dim3(TILE), 0, s, a);
-				return hipGetLastError();
-			case 8:
-				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 8>), dim3(grid), dim3(TILE), 0, s, a);
-				return hipGetLastError();
-			case 12:
-				hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 12>), dim3(grid), dim3(TILE), 0, s, a);
-				return hipGetLastError();
-#define XFG_XV(x)                                                                              \
-			case x:                                                                \
-				hipLaunchKernelGGL((xfg_classify_kernel<FEAT | x, 64, 0>), dim3(grid), \
-						   dim3(TILE), 0, s, a);                       \
-				return hipGetLastError();
-			XFG_XV(0x100) XFG_XV(0x200) XFG_XV(0x400) XFG_XV(0x800) XFG_XV(0xF00)
-#undef XFG_XV
-			default:
-				break;
+					hipLaunchKernelGGL((xfg_pipe4_kernel<FEAT, 128, false>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
 			}
 		}
-		if (a.dense)
-			hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 0, true>), dim3(grid), dim3(TILE), dl, s, a);
-		else
-			hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64, 0>), dim3(grid), dim3(TILE), dl, s, a);
+		if (!done) {
+			if (a.window <= 64 && a.dense)
+				hipLaunchKernelGGL((xfg_pipeline_kernel<FEAT, 64, true, 0>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
+			else if (a.window <= 64)
+				hipLaunchKernelGGL((xfg_pipeline_kernel<FEAT, 64, false, 0>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
+			else if (a.dense)
+				hipLaunchKernelGGL((xfg_pipeline_kernel<FEAT, 128, true, 0>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
+			else
+				hipLaunchKernelGGL((xfg_pipeline_kernel<FEAT, 128, false, 0>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
+		}
+	} else if (a.window <= 64) {
+		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 64>), dim3(grid), dim3(TILE), dl, s, a);
 	} else {
-		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128, 0>), dim3(grid), dim3(TILE), dl, s, a);
+		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128>), dim3(grid), dim3(TILE), dl, s, a);
 	}
 	hipError_t e = hipGetLastError();
-	if (e != hipSuccess || !a.hlog)
+	if (e != hipSuccess || !a.tlog)
 		return e;
-	hipLaunchKernelGGL(xfg_hlog_count_kernel, dim3(a.hlog_parts), dim3(HC_THREADS), 0, s, a, grid);
+	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS), dim3(LC_THREADS),
+			   (size_t)a.log_hist * 4, s, a, a.log_hist);
 	return hipGetLastError();
 }
 
@@ -1574,47 +1143,57 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 	return e == hipSuccess ? 0 : -(int)e - 1000;
 }
 
-// Resident workgroups per CU of the classify kernel a launch would use
-// (grid sizing: one persistent wave of workgroups); window 1 = the streamed
-// kernel, 2 / 3 = the pipelined kernel with a 64 / 128-byte window.
+// Resident workgroups per CU of a classify kernel (persistent grid sizing)
+// with `dyn` bytes of dynamic LDS: kind 0 = general, 1 = pipelined (key
+// mode 0), 2 = pipelined (key mode 1); window 64 or 128.
 template <uint32_t FEAT>
-static int occupancy_feat(uint32_t window)
+static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 {
 	int n = 0;
+	hipError_t e = hipSuccess;
+	bool done = false;
 	if constexpr ((FEAT & F_IPV4) != 0) {
-		if (window == 4) {
-			hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-				&n, xfg_classify_spec_kernel<FEAT, 64, true>, TILE, 1024);
-			return e == hipSuccess && n > 0 ? n : 4;
+		if (kind == 2) {
+			done = true;
+			e = window <= 64
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 64, true>, PIPE_THREADS(64), dyn)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 128, false>, PIPE_THREADS(128), dyn);
 		}
 	}
-	hipError_t e = window == 2 || window == 4
-		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_pipe_kernel<FEAT, 64, true>, TILE, 0)
-		: window == 3
-		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_pipe_kernel<FEAT, 128, false>, TILE, 0)
-		: window == 1
-		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_stream_kernel<FEAT, 0>, IO_THREADS, 0)
-		: window <= 64
-		? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_kernel<FEAT, 64, 0, true>, TILE, 0)
-		: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_kernel<FEAT, 128, 0>, TILE, 0);
-	return e == hipSuccess && n > 0 ? n : 4;
+	if (done)
+		;
+	else if (kind >= 1)
+		e = window <= 64
+			? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeline_kernel<FEAT, 64, true, 0>, PIPE_THREADS(64), dyn)
+			: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeline_kernel<FEAT, 128, false, 0>, PIPE_THREADS(128), dyn);
+	else
+		e = window <= 64
+			? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_kernel<FEAT, 64>, TILE, dyn)
+			: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_classify_kernel<FEAT, 128>, TILE, dyn);
+	return e == hipSuccess && n > 0 ? n : 1;
 }
 
-extern "C" int xfg_classify_occupancy(uint32_t prog_features, uint32_t window)
+extern "C" int xfg_classify_occupancy(uint32_t prog_features, int kind, uint32_t window, size_t dyn)
 {
 	switch (prog_features) {
-	case F_UDP | F_DENY:              return occupancy_feat<F_UDP | F_DENY>(window);
-	case F_TCP | F_DENY:              return occupancy_feat<F_TCP | F_DENY>(window);
-	case F_IPV4 | F_IPV6 | F_DENY:    return occupancy_feat<F_IPV4 | F_IPV6 | F_DENY>(window);
-	case F_ETH | F_DENY:              return occupancy_feat<F_ETH | F_DENY>(window);
-	case XFG_ALL | F_DENY:            return occupancy_feat<XFG_ALL | F_DENY>(window);
-	case F_UDP | XFG_ALLOW:           return occupancy_feat<F_UDP | XFG_ALLOW>(window);
-	case F_TCP | XFG_ALLOW:           return occupancy_feat<F_TCP | XFG_ALLOW>(window);
-	case F_IPV4 | F_IPV6 | XFG_ALLOW: return occupancy_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(window);
-	case F_ETH | XFG_ALLOW:           return occupancy_feat<F_ETH | XFG_ALLOW>(window);
-	case XFG_ALL | XFG_ALLOW:         return occupancy_feat<XFG_ALL | XFG_ALLOW>(window);
-	default:                          return 4;
+	case F_UDP | F_DENY:              return occupancy_feat<F_UDP | F_DENY>(kind, window, dyn);
+	case F_TCP | F_DENY:              return occupancy_feat<F_TCP | F_DENY>(kind, window, dyn);
+	case F_IPV4 | F_IPV6 | F_DENY:    return occupancy_feat<F_IPV4 | F_IPV6 | F_DENY>(kind, window, dyn);
+	case F_ETH | F_DENY:              return occupancy_feat<F_ETH | F_DENY>(kind, window, dyn);
+	case XFG_ALL | F_DENY:            return occupancy_feat<XFG_ALL | F_DENY>(kind, window, dyn);
+	case F_UDP | XFG_ALLOW:           return occupancy_feat<F_UDP | XFG_ALLOW>(kind, window, dyn);
+	case F_TCP | XFG_ALLOW:           return occupancy_feat<F_TCP | XFG_ALLOW>(kind, window, dyn);
+	case F_IPV4 | F_IPV6 | XFG_ALLOW: return occupancy_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(kind, window, dyn);
+	case F_ETH | XFG_ALLOW:           return occupancy_feat<F_ETH | XFG_ALLOW>(kind, window, dyn);
+	case XFG_ALL | XFG_ALLOW:         return occupancy_feat<XFG_ALL | XFG_ALLOW>(kind, window, dyn);
+	default:                          return 1;
 	}
+}
+
+// Threads per workgroup of a classify kernel (host grid sizing).
+extern "C" int xfg_classify_threads(int kind, uint32_t window)
+{
+	return kind >= 1 ? (window <= 64 ? PIPE_THREADS(64) : PIPE_THREADS(128)) : TILE;
 }
 
 // Streaming-read probe: the achievable HBM read rate on this device, used by

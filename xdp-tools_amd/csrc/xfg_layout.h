@@ -33,7 +33,7 @@
  * once placed, so slot indices (and the per-device counters) are stable
  * across inserts and deletes.
  *
- * Prefilter: a blocked Bloom filter of 64-bit words (one word per key, 4
+ * Prefilter: a blocked Bloom filter of 32-bit words (one word per key, 4
  * bits from a second hash) answers most negative lookups from a table small
  * enough to stay in each XCD's L2.  Deleted keys leave their bits set
  * (false positives only; the bucket probe decides), and the host rebuilds
@@ -58,23 +58,21 @@
 
 #define XFG_META_OVERFLOW 1u
 
-#define XFG_PROF_WG 8192u  /* diagnostics: workgroups with a phase-cycle record */
-
 #define XFG_PORT_TAB      2048u   /* LDS port table slots (8 KiB, the bitmap's size) */
 #define XFG_PORT_TAB_MAX  1024u   /* at most this many ruled ports use the table */
+#define XFG_PORT_NIB_WORDS 8192u  /* more: every port's 4 flag bits, 32 KiB of LDS */
 
 #define XFG_BLOOM_K       4u
 
-#define XFG_HLOG_SHIFT    14u     /* hit-log partition: 16384 counters (64 KiB of LDS) */
-#define XFG_HLOG_PARTS_MAX 4096u  /* partitions a classify workgroup can track */
 #define XFG_DCNT_MAX      4096u   /* direct LDS counters (16 KiB) */
-#define XFG_SLOG_SHIFT    10u     /* speculative records: 1024 bucket lines per partition */
+#define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
+#define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
 
 
 /* Per-hash-map descriptor passed to the kernel by value. */
 struct xfg_tdesc {
 	const void *buckets;         /* (nbuckets + 1) * 64 B */
-	const unsigned long long *bloom; /* bloom_words x u64 */
+	const uint32_t *bloom;       /* bloom_words x u32 */
 	unsigned long long *hits;    /* nslots + 1 */
 	uint32_t nbuckets;
 	uint32_t max_disp;
@@ -90,8 +88,6 @@ struct xfg_tdesc {
 /* Kernel arguments of one classify launch. */
 struct xfg_kargs {
 	struct xfg_tdesc t4, t6, te;
-	const uint8_t *port_flags;
-	const uint32_t *port_bits;    /* 65536-bit "flags != 0" bitmap */
 	unsigned long long *port_hits;
 	uint32_t port_count;          /* ports with non-zero flags; 0 => skip */
 	uint32_t window;              /* header window staged in LDS (64 or 128) */
@@ -103,20 +99,16 @@ struct xfg_kargs {
 	uint32_t stride;
 	uint32_t lens_u16;
 	uint8_t *verdicts;
-	uint32_t ablate;              /* diagnostics only (XFG_ABLATE env), 0 in production:
-				       * 2 = no counter atomics, 4 = stage only (no parse) */
-	uint32_t variant;             /* diagnostics only (XFG_VARIANT env): build variant */
 	uint32_t port_fmask;          /* OR of the port flag bytes (see tdesc.fmask) */
-	uint32_t streamed;            /* 1: the streamed kernel (I/O wave + lookup waves) */
-	unsigned long long *prof;     /* diagnostics: per-workgroup phase cycles (variant 4) */
-	/* Ruled ports as a small open-addressed table each workgroup copies to
-	 * LDS (NULL when more than XFG_PORT_TAB_MAX ports carry flags: then the
-	 * bitmap above plus a port_flags read) */
+	/* The ruled ports, as each workgroup copies them to LDS: a small
+	 * open-addressed table (at most XFG_PORT_TAB_MAX ports carry flags), or
+	 * else (port_tab NULL) the nibble map of all 65536 ports' flags */
 	const uint32_t *port_tab;     /* XFG_PORT_TAB entries: flags << 16 | key, 0 = empty */
 	uint32_t port_tab_disp;       /* longest probe displacement in the table */
-	/* Global counter index space (the LDS counter cache's tags): v4 slots,
-	 * v6 slots, eth slots (each with its zero-key slot), then the 65536
-	 * ports; gbase[i] = first index of each. */
+	const uint32_t *port_nib;     /* XFG_PORT_NIB_WORDS: port k's flags at bits 4(k%8) of word k/8 */
+	/* Global counter index space (counter identities): v4 slots, v6 slots,
+	 * eth slots (each with its zero-key slot), then the 65536 ports;
+	 * gbase[i] = first index of each. */
 	uint32_t gbase[4];
 	/* AF_XDP descriptors (xfg_classify_descs): packet i is record
 	 * (desc_first + i) & desc_mask of an array of struct xdp_desc {u64 addr;
@@ -125,32 +117,25 @@ struct xfg_kargs {
 	const uint64_t *descs;
 	uint32_t desc_mask;
 	uint32_t desc_first;
-	uint32_t dense;               /* stride == window, no offsets/descriptors */
+	uint32_t dense;               /* pipelined kernel: stride == window */
 	uint32_t pipe;                /* the pipelined kernel (fixed stride >= window) */
-	uint32_t fix_cap;             /* pipelined: deferred-packet list entries per wave */
-	uint32_t *fix_list;           /* pipelined: (grid * 4) lists of fix_cap entries */
-	/* Hit log (pipelined kernel; NULL = memory-side atomics): the counter
-	 * identities of cold hits, partitioned by identity >> XFG_HLOG_SHIFT.
-	 * Workgroup w appends to region (p * grid + w) * hlog_cap of partition p
-	 * and leaves its fill in hlog_cnt[p * grid + w]; xfg_hlog_count_kernel
-	 * sums each partition in LDS into the counters. */
-	uint32_t *hlog;
-	uint32_t *hlog_cnt;
-	uint32_t hlog_cap;
-	uint32_t hlog_parts;
-	/* Classic kernel, small rule sets: the counters with identity < dcnt
-	 * (all hash maps, gbase[3], or the IPv4 map, gbase[1]) have a direct LDS
-	 * slot per workgroup, flushed once; 0 = off */
+	uint32_t km;                  /* pipelined key mode: 1 = only IPv4 keys are live */
+	/* Direct LDS counters: identities below dcnt (all hash maps, gbase[3],
+	 * or the IPv4 map, gbase[1]) are summed per workgroup in LDS; 0 = off */
 	uint32_t dcnt;
-	/* Speculative single-lookup mode (xfg_spec.hip): 16-byte records per
-	 * (partition of 2^XFG_SLOG_SHIFT home buckets, workgroup), same layout
-	 * as the hit log; spec = 0 when the rule set has more than one live
-	 * lookup per packet. */
-	void *slog;
-	uint32_t *slog_cnt;
-	uint32_t slog_cap;
-	uint32_t slog_parts;
-	uint32_t spec;
+	/* Hit log of the pipelined kernels (tlog NULL = no log): per-wave
+	 * regions of defer_cap counter identities; partition-major buffer of
+	 * XFG_LOG_PARTS x pcap entries with fills pfill[]; the count kernel's
+	 * LDS histogram has log_hist entries (xfg_kernels.hip, HitLog). */
+	uint32_t *tlog;
+	uint32_t *pbuf;
+	uint32_t *pfill;
+	uint32_t pcap;
+	uint32_t log_hist;
+	/* Pipelined kernel: deferred packets, defer_cap entries per wave */
+	uint32_t *defer;
+	uint32_t defer_cap;
+	uint32_t diag;                /* diagnostics build only (XFG_DIAG_MASK); 0 */
 };
 
 
@@ -202,11 +187,11 @@ XFG_HD uint32_t xfg_bloom_word(uint32_t h, uint32_t nwords)
 	return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * nwords) >> 32);
 }
 
-XFG_HD unsigned long long xfg_bloom_mask(uint32_t h)
+XFG_HD uint32_t xfg_bloom_mask(uint32_t h)
 {
 	uint32_t g = xfg_fmix32(h ^ 0x7f4a7c15u);
-	return (1ull << (g & 63)) | (1ull << ((g >> 6) & 63)) | (1ull << ((g >> 12) & 63)) |
-	       (1ull << ((g >> 18) & 63));
+	return (1u << (g & 31)) | (1u << ((g >> 5) & 31)) | (1u << ((g >> 10) & 31)) |
+	       (1u << ((g >> 15) & 31));
 }
 
 /* Home slot of a port key in the LDS port table. */

@@ -39,10 +39,10 @@ int xfg_table_init(struct xfg_table *t, uint32_t keylen, uint32_t capacity, uint
 	if (t->nslots >= (1u << 30))   /* kernel counter tags carry 30-bit slots */
 		return -E2BIG;
 	/* ~12 filter bits per key: a 1M-rule filter is 1.5 MB (L2-resident) */
-	uint64_t words = ((uint64_t)capacity * 12 + 63) / 64;
-	t->bloom_words = (uint32_t)(words < 16 ? 16 : words);
+	uint64_t words = ((uint64_t)capacity * 12 + 31) / 32;
+	t->bloom_words = (uint32_t)(words < 32 ? 32 : words);
 	t->img = calloc(xfg_table_img_bytes(t), 1);
-	t->bloom = calloc(t->bloom_words, 8);
+	t->bloom = calloc(t->bloom_words, 4);
 	if (!t->img || !t->bloom) {
 		xfg_table_free(t);
 		return -ENOMEM;
@@ -192,7 +192,7 @@ int xfg_table_bloom_needs_rebuild(const struct xfg_table *t)
 
 void xfg_table_bloom_rebuild(struct xfg_table *t)
 {
-	memset(t->bloom, 0, (size_t)t->bloom_words * 8);
+	memset(t->bloom, 0, (size_t)t->bloom_words * 4);
 	for (uint64_t s = 0; s < t->nslots; s++) {
 		const uint8_t *k = t->img + xfg_table_key_off(t, s);
 		if (!is_zero(k, t->slot_bytes))

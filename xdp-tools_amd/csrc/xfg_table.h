@@ -26,7 +26,7 @@ struct xfg_table {
 	uint32_t bloom_words;
 	uint32_t bloom_stale; /* deletes since the filter was last rebuilt */
 	uint8_t *img;         /* (nbuckets + 1) * 64 bytes: keys + meta, flags zero */
-	unsigned long long *bloom;
+	uint32_t *bloom;
 };
 
 /* keylen 4 (ipv4), 16 (ipv6), 6 (ethernet). Returns 0 or -ENOMEM/-EINVAL. */

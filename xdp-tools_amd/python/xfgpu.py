@@ -26,7 +26,10 @@ except Exception:  # torch absent: the library uses /opt/rocm's runtime
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libxdpfilter_gpu.so")
+# XFG_LIB=diag selects the diagnostics build (measurement knobs; tools/ only)
+LIB_PATH = os.path.join(os.path.dirname(HERE), "lib",
+                        "libxdpfilter_gpu_diag.so" if os.environ.get("XFG_LIB") == "diag"
+                        else "libxdpfilter_gpu.so")
 
 FEAT_TCP, FEAT_UDP, FEAT_IPV6, FEAT_IPV4, FEAT_ETHERNET = 1, 2, 4, 8, 16
 FEAT_ALL = 31
