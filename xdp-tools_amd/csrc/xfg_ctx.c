@@ -997,7 +997,7 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	 * be loaded without a length (stride >= window, 16-byte aligned; packet
 	 * indices fit its 32-bit deferred lists); the general kernel the rest. */
 	a->pipe = !b->offsets && b->stride >= a->window && !(b->stride & 15) &&
-		  !((uintptr_t)b->data & 15) && b->count < (1ull << 32);
+		  !((uintptr_t)b->data & 15) && b->count < (1ull << 32) && b->stride < 65536;
 #ifdef XFG_DIAG
 	const char *ks = getenv("XFG_KERNEL");   /* diagnostics build only */
 	if (ks && !strcmp(ks, "general"))

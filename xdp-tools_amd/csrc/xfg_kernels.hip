@@ -828,26 +828,47 @@ struct Counters {
 __device__ __forceinline__ uint32_t log_part(uint32_t g) { return (g >> 4) & (XFG_LOG_PARTS - 1); }
 __device__ __forceinline__ uint32_t log_local(uint32_t g) { return ((g >> 12) << 4) | (g & 15); }
 
+// Set bits of the wave mask m below this lane (mbcnt: no lane mask register).
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m)
+{
+	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ void log_append(uint32_t *region, uint32_t &cnt, uint32_t tag, int lane)
 {
 	const unsigned long long m = __ballot(tag != CT_NONE);
 	if (m) {
 		if (tag != CT_NONE)
-			region[cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = tag;
+			region[cnt + lanes_below(m)] = tag;
 		cnt += (uint32_t)__popcll(m);
 	}
 }
 
 // Workgroup end: the NW wave regions (counts in s_n) into the partition
-// buffers.  s_h, s_b: LDS scratch of XFG_LOG_PARTS words each.  Whole
-// workgroup, after a barrier.
+// buffers.  Two passes over the regions: an LDS histogram, one reservation
+// per partition in its buffer (pfill), then chunks of LOG_CHUNK entries
+// counting-sorted by partition in LDS and written out as per-partition runs
+// (consecutive lanes, consecutive addresses).  s: LDS scratch of
+// 4 * XFG_LOG_PARTS + LOG_CHUNK words.  Whole workgroup, after a barrier.
+constexpr uint32_t LOG_CHUNK = 2048;
+
 template <int NW>
-__device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t *s_n, uint32_t *s_h,
-					      uint32_t *s_b, int tid, int nthr)
+__device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t *s_n, uint32_t *s,
+					      int tid)
 {
+	constexpr int NTH = 64 * NW, K = LOG_CHUNK / NTH;
+	static_assert(LOG_CHUNK % NTH == 0, "chunk: whole entries per thread");
+	const int nthr = NTH;
+	uint32_t *const s_h = s;                         // histogram, then the chunk's counts
+	uint32_t *const s_b = s + XFG_LOG_PARTS;         // the workgroup's slice of each buffer
+	uint32_t *const s_cur = s + 2 * XFG_LOG_PARTS;   // entries written per partition
+	uint32_t *const s_off = s + 3 * XFG_LOG_PARTS;   // the chunk's run starts
+	uint32_t *const s_srt = s + 4 * XFG_LOG_PARTS;   // the chunk, sorted
 	const uint64_t r0 = (uint64_t)blockIdx.x * NW * a.defer_cap;
-	for (int i = tid; i < (int)XFG_LOG_PARTS; i += nthr)
+	for (int i = tid; i < (int)XFG_LOG_PARTS; i += nthr) {
 		s_h[i] = 0;
+		s_cur[i] = 0;
+	}
 	__syncthreads();
 	for (int w = 0; w < NW; w++) {
 		const uint32_t *reg = a.tlog + r0 + (uint64_t)w * a.defer_cap;
@@ -858,18 +879,66 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 	for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
 		const uint32_t c = s_h[p];
 		s_b[p] = c ? atomicAdd(&a.pfill[p], c) : 0;
-		s_h[p] = 0;   // now the cursor
+		s_h[p] = 0;
 	}
 	__syncthreads();
+	const int lane = tid & 63;
 	for (int w = 0; w < NW; w++) {
 		const uint32_t *reg = a.tlog + r0 + (uint64_t)w * a.defer_cap;
-		for (uint32_t e = tid; e < s_n[w]; e += nthr) {
-			const uint32_t g = reg[e], p = log_part(g);
-			const uint32_t pos = s_b[p] + atomicAdd(&s_h[p], 1u);
-			if (pos < a.pcap)
-				a.pbuf[(uint64_t)p * a.pcap + pos] = g;
-			else
-				atomicAdd(global_counter(a, g), 1ull);
+		const uint32_t nw = s_n[w];
+		for (uint32_t c0 = 0; c0 < nw; c0 += LOG_CHUNK) {
+			const uint32_t cn = min(LOG_CHUNK, nw - c0);
+			// rank each entry within its partition
+			uint32_t g[K], rk[K];
+#pragma unroll
+			for (int j = 0; j < K; j++) {
+				const uint32_t e = tid + j * NTH;
+				g[j] = e < cn ? reg[c0 + e] : CT_NONE;
+				rk[j] = g[j] != CT_NONE ? atomicAdd(&s_h[log_part(g[j])], 1u) : 0u;
+			}
+			__syncthreads();
+			// run starts: exclusive scan of the counts (one wave)
+			if (tid < 64) {
+				uint32_t v[XFG_LOG_PARTS / 64], sum = 0;
+#pragma unroll
+				for (int q = 0; q < (int)(XFG_LOG_PARTS / 64); q++) {
+					v[q] = s_h[lane * (XFG_LOG_PARTS / 64) + q];
+					sum += v[q];
+				}
+				uint32_t inc = sum;
+#pragma unroll
+				for (int o = 1; o < 64; o <<= 1) {
+					const uint32_t y = __shfl_up(inc, o);
+					if (lane >= o)
+						inc += y;
+				}
+				uint32_t run = inc - sum;
+#pragma unroll
+				for (int q = 0; q < (int)(XFG_LOG_PARTS / 64); q++) {
+					s_off[lane * (XFG_LOG_PARTS / 64) + q] = run;
+					run += v[q];
+				}
+			}
+			__syncthreads();
+#pragma unroll
+			for (int j = 0; j < K; j++)
+				if (g[j] != CT_NONE)
+					s_srt[s_off[log_part(g[j])] + rk[j]] = g[j];
+			__syncthreads();
+			for (uint32_t t = tid; t < cn; t += nthr) {
+				const uint32_t x = s_srt[t], p = log_part(x);
+				const uint32_t pos = s_b[p] + s_cur[p] + (t - s_off[p]);
+				if (pos < a.pcap)
+					a.pbuf[(uint64_t)p * a.pcap + pos] = x;
+				else
+					atomicAdd(global_counter(a, x), 1ull);
+			}
+			__syncthreads();
+			for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
+				s_cur[p] += s_h[p];
+				s_h[p] = 0;
+			}
+			__syncthreads();
 		}
 	}
 }

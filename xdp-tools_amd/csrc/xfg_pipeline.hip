@@ -538,7 +538,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 			stat(w_act, w_len);
 			const unsigned long long dm = __ballot(w_act == A_DEFER);
 			if (dm) {
-				const uint32_t pos = ndef + (uint32_t)__popcll(dm & ((1ull << lane) - 1));
+				const uint32_t pos = ndef + lanes_below(dm);
 				if (w_act == A_DEFER)
 					dlist[pos] = gi;
 				ndef += (uint32_t)__popcll(dm);
@@ -682,8 +682,9 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
 	cn.flush(a, tid, NT);
+	static_assert(NW * 64 * ROWDW >= 4 * XFG_LOG_PARTS + LOG_CHUNK, "partition scratch");
 	if (a.tlog)   // (win is free now: the partition scratch)
-		log_partition<NW>(a, s_tn, win, win + XFG_LOG_PARTS, tid, NT);
+		log_partition<NW>(a, s_tn, win, tid);
 }
 
 }  // namespace
@@ -702,6 +703,14 @@ struct Parse4 {
 	bool v4ok, defer;
 };
 
+// Branch-free helpers: every operand evaluated, combined with bitwise
+// operators (short-circuit && / || and ?: chains over one value get turned
+// into switch trees of divergent branches).
+__device__ __forceinline__ uint32_t pick(bool c, uint32_t x, uint32_t y)
+{
+	return y ^ ((x ^ y) & (0u - (uint32_t)c));
+}
+
 template <uint32_t FEAT, int W>
 __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 {
@@ -713,7 +722,7 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	const uint32_t et = d3 & 0xffff;   // raw (network-order) ethertype
 	const bool runt = len < 14;        // parse_ethhdr
 	const bool is4 = et == 0x0008, is6 = et == 0xdd86;
-	const bool vlan = et == 0x0081 || et == 0xa888;
+	const bool vlan = (et == 0x0081) | (et == 0xa888);
 	const bool arp = et == 0x0608;
 	// IPv4 (__parse_iphdr, frags ok, no version check): ihl 5 keeps L4 at 34
 	const bool s4 = len < 34;
@@ -722,35 +731,64 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	const bool u4 = (FEAT & F_UDP) && proto == 17, t4 = (FEAT & F_TCP) && proto == 6;
 	const uint32_t ulen4 = ((d9 >> 8) & 0xff00) | (d9 >> 24);
 	const uint32_t doff4 = (d11 >> 20) & 0xf;
-	const bool ab4 = u4 ? (len < 42 || ulen4 < 8) : t4 ? (len < 54 || 34 + doff4 * 4 > len) : false;
-	// IPv6 (__parse_ip6hdr + skip_ip6hdrext): a final next header at 54
+	const bool ab4 = (u4 & ((len < 42) | (ulen4 < 8))) | (t4 & ((len < 54) | (34 + doff4 * 4 > len)));
+	// IPv6 (__parse_ip6hdr + skip_ip6hdrext): a final next header at 54;
+	// extension headers 0, 43, 44, 51, 58 (as the walk treats it), 60, 135
 	const uint32_t nh = d5 & 0xff;
-	const bool ext = nh == 0 || nh == 60 || nh == 43 || nh == 135 || nh == 51 || nh == 44 ||
-			 nh == 58;
+	constexpr uint64_t EXT = (1ull << 0) | (1ull << 43) | (1ull << 44) | (1ull << 51) | (1ull << 58) |
+				 (1ull << 60);
+	const bool ext = ((nh < 64) & (uint32_t)(EXT >> (nh & 63))) | (nh == 135);
 	const bool s6 = len < 56;          // len < 54 (header) or the walk's read at 54
 	const bool u6 = (FEAT & F_UDP) && nh == 17, t6 = (FEAT & F_TCP) && nh == 6;
 	const uint32_t ulen6 = ((d14 >> 8) & 0xff00) | (d14 >> 24);
 	const uint32_t doff6 = (d16 >> 20) & 0xf;
-	const bool t6far = W < 68 && t6 && len >= 74;   // doff at byte 66: past the window
-	const bool ab6 = u6 ? (len < 62 || ulen6 < 8) : t6 ? (len < 74 || 54 + doff6 * 4 > len) : false;
+	const bool t6far = (W < 68) & t6 & (len >= 74);   // doff at byte 66: past the window
+	const bool ab6 = (u6 & ((len < 62) | (ulen6 < 8))) | (t6 & ((len < 74) | (54 + doff6 * 4 > len)));
 	Parse4 r;
-	r.defer = !runt && (vlan || arp || (is4 && !s4 && !ihl5) || (is6 && !s6 && (ext || t6far)));
-	r.abort_at = runt ? ST_ETH
-		   : is4 ? (s4 ? ST_IP : ab4 ? ST_L4 : NST)
-		   : is6 ? (s6 ? ST_IP : ab6 ? ST_L4 : NST)
-		   : NST;
-	const uint32_t l4 = is4 ? (u4 ? 17u : t4 ? 6u : 0u) : is6 ? (u6 ? 17u : t6 ? 6u : 0u) : 0u;
-	r.l4proto = r.abort_at == NST ? l4 : 0u;
-	r.psrc = is4 ? d8 >> 16 : d13 >> 16;
-	r.pdst = is4 ? d9 & 0xffff : d14 & 0xffff;
+	r.defer = !runt & (vlan | arp | (is4 & !s4 & !ihl5) | (is6 & !s6 & (ext | t6far)));
+	const bool sip = (is4 & s4) | (is6 & s6);          // short IP header
+	const bool sl4 = (is4 & !s4 & ab4) | (is6 & !s6 & ab6);
+	r.abort_at = pick(runt, ST_ETH, pick(sip, ST_IP, pick(sl4, ST_L4, NST)));
+	const uint32_t l4 = pick(is4, pick(u4, 17u, pick(t4, 6u, 0u)), pick(is6, pick(u6, 17u, pick(t6, 6u, 0u)), 0u));
+	r.l4proto = pick(r.abort_at == NST, l4, 0u);
+	r.psrc = pick(is4, d8 >> 16, d13 >> 16);
+	r.pdst = pick(is4, d9 & 0xffff, d14 & 0xffff);
 	r.k4a = __builtin_amdgcn_alignbyte(d8, d7, 2);   // daddr 30..33
 	r.k4b = __builtin_amdgcn_alignbyte(d7, d6, 2);   // saddr 26..29
-	r.v4ok = !runt && is4 && !s4;
+	r.v4ok = !runt & is4 & !s4;
 	return r;
+}
+
+// The port rule of `key` in the workgroup's LDS copy: its flags, and with
+// the open-addressed table its slot (the workgroup's direct counter for
+// it; XFG_PORT_TAB with the nibble map).  The probe runs the table's
+// longest displacement for every lane (keys are unique, so at most one
+// slot matches).
+__device__ __forceinline__ uint32_t port_probe(const uint32_t *s_ports, bool tab, uint32_t disp,
+					       uint32_t key, uint32_t &slot)
+{
+	slot = XFG_PORT_TAB;
+	if (!tab)
+		return (s_ports[key >> 3] >> ((key & 7) * 4)) & 15;
+	uint32_t f = 0, sl = xfg_port_slot(key);
+	for (uint32_t d = 0; d <= disp; d++) {
+		const uint32_t e = s_ports[sl];
+		const bool m = (e != 0) & ((e & 0xffff) == key);
+		f = pick(m, e >> 16, f);
+		slot = pick(m, sl, slot);
+		sl = (sl + 1) & (XFG_PORT_TAB - 1);
+	}
+	return f;
 }
 
 // bits of the per-packet key flags
 constexpr uint32_t KF_A = 1, KF_B = 2, KF_AZ = 4, KF_BZ = 8;
+
+#ifdef XFG_MARK   // ISA study: stage markers in the assembly
+#define PMARK(x) asm volatile("; MARK " x)
+#else
+#define PMARK(x)
+#endif
 
 template <uint32_t FEAT, int W, bool DENSE>
 __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_kernel(const xfg_kargs a)
@@ -765,6 +803,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	__shared__ uint32_t win[NW * 64 * ROWDW];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
+	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB : 1];   // per port-table slot
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
 	__shared__ unsigned long long s_stats[6];
 	extern __shared__ uint32_t s_dyn[];
@@ -774,7 +813,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	// the IPv4 table, in scalar registers
 	const uint32_t nb = rfl(a.t4.nbuckets), md = rfl(a.t4.max_disp), ns = rfl(a.t4.nslots);
 	const uint32_t zp = rfl(a.t4.zero_present), bw = rfl(a.t4.bloom_words);
-	const uint32_t seed = rfl(a.t4.seed), gb = rfl(a.gbase[0]);
+	const uint32_t seed = rfl(a.t4.seed), gb = rfl(a.gbase[0]), gb3 = rfl(a.gbase[3]);
 	const uint64_t bk = rfl64((uint64_t)(uintptr_t)a.t4.buckets);
 	const uint64_t bl = rfl64((uint64_t)(uintptr_t)a.t4.bloom);
 	// live lookups (census): key a = dst if dst rules exist else src; key b
@@ -794,31 +833,50 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	if (tid < 6)
 		s_stats[tid] = 0;
 	const uint32_t *s_ports = stage_ports<FEAT>(a, s_tab, s_dyn, tid, NT);
+	const bool ptab = PORTS && a.port_count && a.port_tab;
+	const uint32_t pdisp = rfl(a.port_tab_disp);
+	if constexpr (PORTS)
+		for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
+			s_pcnt[i] = 0;
 	__syncthreads();
 
 	uint32_t *const rows = win + wv * 64 * ROWDW;
 	const uint32_t *const myrow = rows + lane * ROWDW;
-	uint32_t *const dlist = a.defer + ((uint64_t)blockIdx.x * NW + wv) * a.defer_cap;
-	uint32_t *const tregion = a.tlog + ((uint64_t)blockIdx.x * NW + wv) * a.defer_cap;
+	// (wave-uniform pointers, kept in scalar registers)
+	uint32_t *const dlist = reinterpret_cast<uint32_t *>(
+		rfl64((uint64_t)(uintptr_t)(a.defer + ((uint64_t)blockIdx.x * NW + wv) * a.defer_cap)));
+	uint32_t *const tregion = reinterpret_cast<uint32_t *>(
+		rfl64((uint64_t)(uintptr_t)(a.tlog + ((uint64_t)blockIdx.x * NW + wv) * a.defer_cap)));
 	uint32_t tn = 0;
-	const uint32_t lg_lo = a.dcnt, lg_hi = a.tlog ? a.gbase[3] : 0u;
-	auto count = [&](uint32_t tag) {
-		const bool lg = tag >= lg_lo && tag < lg_hi;
-		log_append(tregion, tn, lg ? tag : CT_NONE, lane);
-		cn.bump(a, lg ? CT_NONE : tag, lane);
+	const uint32_t lg_lo = rfl(a.dcnt), lg_hi = a.tlog ? rfl(a.gbase[3]) : 0u;
+	// a hit's counter: a ruled port's goes to its table slot's LDS counter,
+	// a direct counter's to LDS, a hash-map counter's to the hit log, any
+	// other (the nibble map's ports, the log off) through Counters::bump
+	auto count = [&](uint32_t tag, uint32_t pslot) {
+		const bool ps = pslot < XFG_PORT_TAB;
+		const bool dc = tag < lg_lo;
+		const bool lg = (tag >= lg_lo) & (tag < lg_hi);
+		log_append(tregion, tn, pick(lg, tag, CT_NONE), lane);
+		if constexpr (PORTS)
+			if (ps)
+				atomicAdd(&s_pcnt[pslot], 1u);
+		if (dc & !ps)
+			atomicAdd(&cn.dcnt[tag], 1u);
+		cn.bump(a, pick(lg | dc | ps, CT_NONE, tag), lane);
 	};
 	const uint32_t n = (uint32_t)a.n;
 	const uint32_t nt = (n + 63) / 64;
 	const uint32_t first = blockIdx.x * NW + wv;
 	const uint32_t step = gridDim.x * NW;
+	// per-action packets (wave totals, scalar) and bytes (per lane)
 	uint32_t st_c0 = 0, st_c1 = 0, st_c2 = 0, st_b0 = 0, st_b1 = 0, st_b2 = 0;
 	auto stat = [&](uint32_t act, uint32_t len) {
-		st_c0 += act == A_ABORTED;
-		st_c1 += act == A_DROP;
-		st_c2 += act == A_PASS;
-		st_b0 += act == A_ABORTED ? len : 0u;
-		st_b1 += act == A_DROP ? len : 0u;
-		st_b2 += act == A_PASS ? len : 0u;
+		st_c0 += (uint32_t)__popcll(__ballot(act == A_ABORTED));
+		st_c1 += (uint32_t)__popcll(__ballot(act == A_DROP));
+		st_c2 += (uint32_t)__popcll(__ballot(act == A_PASS));
+		st_b0 += pick(act == A_ABORTED, len, 0u);
+		st_b1 += pick(act == A_DROP, len, 0u);
+		st_b2 += pick(act == A_PASS, len, 0u);
 	};
 	uint32_t ndef = 0;
 
@@ -831,7 +889,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	const bool l16 = a.lens_u16 != 0;
 	const uint32_t lsh = l16 ? 1u : 2u;
 	const uint64_t lb = rfl64((uint64_t)(uintptr_t)a.lens);
-	auto issue = [&](uint32_t t, u32x4 (&pre)[CPP], uint32_t (&plen)[2]) {
+	auto issue = [&](uint32_t t, u32x4 (&pre)[CPP], uint16_t (&plen)[2]) {
 		t = t < nt ? t : nt - 1;
 		const uint32_t base = t * 64;
 		const uint32_t rem = n - base >= 64 ? 64u : n - base;
@@ -844,81 +902,104 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 			pre[it] = __builtin_nontemporal_load(src);
 		}
 		const uint64_t la = lb + ((uint64_t)(base + ((uint32_t)lane < rem ? lane : 0u)) << lsh);
-		plen[0] = gload16(la);
-		plen[1] = gload16(la + (lsh - 1) * 2);
+		plen[0] = *reinterpret_cast<const __attribute__((address_space(1))) uint16_t *>(la);
+		plen[1] = *reinterpret_cast<const __attribute__((address_space(1))) uint16_t *>(la + (lsh - 1) * 2);
 	};
 
+	// per-packet fallback state, packed: action (3 bits), port-table slot
+	// (12), length (17; the pipelined path takes strides below 2^16)
+	auto pk3 = [](uint32_t act, uint32_t ps, uint32_t len) { return act | ps << 3 | len << 15; };
+	auto pk_act = [](uint32_t p) { return p & 7; };
+	auto pk_ps = [](uint32_t p) { return (p >> 3) & 0xfff; };
+	auto pk_len = [](uint32_t p) { return p >> 15; };
 	// P -> Q (tile k-1)
-	uint32_t q_ka = 0, q_kb = 0, q_ha = 0, q_hb = 0, q_wa = 0, q_wb = 0, q_f = 0;
-	uint32_t q_act = A_NONE, q_tag = CT_NONE, q_len = 0;
+	uint32_t q_ka = 0, q_kb = 0, q_wa = 0, q_wb = 0, q_f = 0;
+	uint32_t q_pk = pk3(A_NONE, XFG_PORT_TAB, 0), q_tag = CT_NONE;
 	// Q -> R (tile k-2)
-	Line r_line;
-	r_line.q0 = r_line.q1 = r_line.q2 = r_line.q3 = u32x4{ 0, 0, 0, 0 };
-	uint32_t r_key = 0, r_b = 0, r_mask = 0, r_act = A_NONE, r_tag = CT_NONE, r_len = 0;
+	uint32_t r_key = 0, r_b = 0, r_mask = 0, r_pk = pk3(A_NONE, XFG_PORT_TAB, 0), r_tag = CT_NONE;
 	bool r_sel = false, r_zero = false, r_more = false;
 
 	// One iteration: `cur` holds tile k's windows (issued two iterations
 	// ago), `nxt` tile k+1's (issued one iteration ago, still in flight);
-	// tile k+2's go into `cur` last.  Returns false when the wave is done.
-	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], uint32_t (&curlen)[2]) -> bool {
+	// tile k+2's go into `cur` last.  The wave runs its tiles + 2 iterations
+	// (a fixed trip count: no early-out path for the wait placement to merge).
+	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], uint16_t (&curlen)[2]) {
 		const uint32_t tP = first + k * step;
 		const bool vP = tP < nt;
 		const bool vQ = k >= 1 && tP - step < nt;
 		const bool vR = k >= 2 && tP - 2 * step < nt;
-		if (!vP && !vQ && !vR)
-			return false;
 		// the iteration's one wait: everything but the last tile's windows
 		// (an explicit wait the compiler's own placement sees)
 		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 2) & 15) | (((CPP + 2) >> 4) << 14));
+		asm volatile("" ::: "memory");   // (the LDS-DMA'd lines: read only after the wait)
 
+		PMARK("R");
 		// ---- R: match (CHECK_MAP, xdpfilt_prog.h:56-64) -> verdict, counter
-		uint32_t w_act = A_NONE, w_tag = CT_NONE;
-		const uint32_t w_len = r_len;
+		const uint32_t r_act = pk_act(r_pk), r_ps = pk_ps(r_pk), w_len = pk_len(r_pk);
+		uint32_t w_act = A_NONE, w_tag = CT_NONE, w_ps = r_ps;
 		if (vR) {
+			// the candidate line, LDS-DMA'd by L into the wave's rows
+			// (packet p's at byte 64p)
+			Line r_line;
+			{
+				const u32x4 *lp4 = reinterpret_cast<const u32x4 *>(rows) + lane * 4;
+				r_line.q0 = lp4[0];
+				r_line.q1 = lp4[1];
+				r_line.q2 = lp4[2];
+				r_line.q3 = lp4[3];
+			}
 			const int m = match_v4(r_line, r_key);
-			const int i = r_zero ? 0 : m;
-			const uint32_t fl = r_line.flag(i < 0 ? 0 : i);
-			const bool hit = r_sel && i >= 0 && (fl & r_mask) == r_mask;
-			const uint32_t slot = r_zero ? ns : r_b * XFG_SLOTS_V4 + (uint32_t)i;
-			const bool defer = r_sel && !hit && (r_more || (i < 0 && r_line.overflow() && md));
-			w_act = hit ? HIT : defer ? A_DEFER : r_act;
-			w_tag = hit ? gb + slot : defer ? CT_NONE : r_tag;
+			const bool found = r_zero | (m >= 0);
+			const uint32_t i = pick(r_zero | (m < 0), 0u, (uint32_t)m);
+			const uint32_t fl = r_line.flag((int)i);
+			const bool hit = r_sel & found & ((fl & r_mask) == r_mask);
+			const uint32_t slot = pick(r_zero, ns, r_b * XFG_SLOTS_V4 + i);
+			const bool defer = r_sel & !hit & (r_more | (!found & r_line.overflow() & (md != 0)));
+			w_act = pick(hit, HIT, pick(defer, A_DEFER, r_act));
+			w_tag = pick(hit, gb + slot, pick(defer, CT_NONE, r_tag));
+			w_ps = pick(hit | defer, XFG_PORT_TAB, r_ps);
 		}
 
+		PMARK("W");
 		// ---- W: verdicts, counters, stats, deferrals of tile k-2
 		if (vR) {
 			const uint32_t gi = (tP - 2 * step) * 64 + lane;
 			if (w_act <= A_PASS && !(dg & 8))
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
-			count((dg & 1) ? CT_NONE : w_tag);
+			PMARK("C");
+			count((dg & 1) ? CT_NONE : w_tag, (dg & 1) ? XFG_PORT_TAB : w_ps);
+			PMARK("T");
 			stat(w_act, w_len);
 			const unsigned long long dm = __ballot(w_act == A_DEFER);
 			if (dm) {
-				const uint32_t pos = ndef + (uint32_t)__popcll(dm & ((1ull << lane) - 1));
+				const uint32_t pos = ndef + lanes_below(dm);
 				if (w_act == A_DEFER)
 					dlist[pos] = gi;
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
 
+		PMARK("Q");
 		// ---- Q: tile k-1's Bloom words -> first candidate key, its bucket
 		bool lsel = false;
 		if (vQ) {
+			const uint32_t q_ha = xfg_hash_v4(q_ka, seed), q_hb = xfg_hash_v4(q_kb, seed);
 			const uint32_t bma = xfg_bloom_mask(q_ha), bmb = xfg_bloom_mask(q_hb);
-			const bool ma = (q_f & KF_A) && ((q_f & KF_AZ) ? zp != 0 : (q_wa & bma) == bma);
-			const bool mb = (q_f & KF_B) && ((q_f & KF_BZ) ? zp != 0 : (q_wb & bmb) == bmb);
-			r_sel = ma || mb;
-			r_more = ma && mb;
-			r_key = ma ? q_ka : q_kb;
-			r_zero = ma ? (q_f & KF_AZ) != 0 : (q_f & KF_BZ) != 0;
-			r_mask = ma ? mask_a : M_SRC;
-			r_b = r_zero ? nb : xfg_home(ma ? q_ha : q_hb, nb);
-			r_act = q_act;
+			const bool za = (q_f & KF_AZ) != 0, zb = (q_f & KF_BZ) != 0;
+			const bool ma = ((q_f & KF_A) != 0) & (za ? zp != 0 : (q_wa & bma) == bma);
+			const bool mb = ((q_f & KF_B) != 0) & (zb ? zp != 0 : (q_wb & bmb) == bmb);
+			r_sel = ma | mb;
+			r_more = ma & mb;
+			r_key = pick(ma, q_ka, q_kb);
+			r_zero = ma ? za : zb;
+			r_mask = pick(ma, mask_a, M_SRC);
+			r_b = pick(r_zero, nb, xfg_home(pick(ma, q_ha, q_hb), nb));
+			r_pk = q_pk;
 			r_tag = q_tag;
-			r_len = q_len;
 			lsel = r_sel;
 		}
 
+		PMARK("S");
 		// ---- S: tile k's windows into the LDS rows (past the batch's
 		// end: zeroes), its lengths clamped to the stride (the slot is the
 		// frame's buffer)
@@ -937,40 +1018,58 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 				dst[2] = ok ? cur[it].z : 0u;
 				dst[3] = ok ? cur[it].w : 0u;
 			}
-			const uint32_t l = l16 ? curlen[0] : curlen[0] | curlen[1] << 16;
+			const uint32_t l = l16 ? (uint32_t)curlen[0] : (uint32_t)curlen[0] | (uint32_t)curlen[1] << 16;
 			len = (uint32_t)lane < rem ? min(l, a.stride) : 0u;
 			__builtin_amdgcn_wave_barrier();
 		}
 
+		PMARK("P");
 		// ---- P: parse tile k, its keys, its fallback; Bloom words issued
 		if (vP) {
 			const uint32_t gi = tP * 64 + lane;
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
-			const bool ka = valid && !r.defer && r.v4ok && (dlive || slive);
-			const bool kb = valid && !r.defer && r.v4ok && dlive && slive;
+			const bool kok = valid & !r.defer & r.v4ok;
+			const bool ka = kok & (dlive | slive);
+			const bool kb = kok & dlive & slive;
 			q_ka = dlive ? r.k4a : r.k4b;
 			q_kb = r.k4b;
-			q_ha = xfg_hash_v4(q_ka, seed);
-			q_hb = xfg_hash_v4(q_kb, seed);
-			q_f = (ka ? KF_A : 0u) | (kb ? KF_B : 0u) | (q_ka == 0 ? KF_AZ : 0u) |
-			      (q_kb == 0 ? KF_BZ : 0u);
+			const uint32_t q_ha = xfg_hash_v4(q_ka, seed), q_hb = xfg_hash_v4(q_kb, seed);
+			q_f = pick(ka, KF_A, 0u) | pick(kb, KF_B, 0u) | pick(q_ka == 0, KF_AZ, 0u) |
+			      pick(q_kb == 0, KF_BZ, 0u);
 			// fallback: ABORTED at a failed check, else the port stage
-			uint32_t fa = r.abort_at != NST ? A_ABORTED : MISS, ft = CT_NONE;
+			// (dst then src, xdpfilt_prog.h:268-301; l4proto is 0 unless the
+			// parse reached a UDP/TCP header)
+			uint32_t fa = pick(r.abort_at != NST, A_ABORTED, MISS), ft = CT_NONE, fs = XFG_PORT_TAB;
 			if constexpr (PORTS) {
-				if (a.port_count && r.l4proto && r.abort_at == NST) {
-					const uint32_t pm = r.l4proto == 17 ? M_UDP : M_TCP;
-					uint32_t t = CT_NONE;
-					if (check_port(a, s_ports, r.pdst, M_DST | pm, t) ||
-					    check_port(a, s_ports, r.psrc, M_SRC | pm, t)) {
-						fa = HIT;
-						ft = t;
+				if (a.port_count) {
+					const uint32_t pm = pick(r.l4proto == 17, M_UDP, M_TCP);
+					const uint32_t pfm = a.port_fmask;
+					bool ph = false;
+					if (can_hit(pfm, M_DST)) {
+						uint32_t sl;
+						const uint32_t f = port_probe(s_ports, ptab, pdisp, r.pdst, sl);
+						const uint32_t mk = M_DST | pm;
+						ph = (r.l4proto != 0) & ((f & mk) == mk) & can_hit(pfm, mk);
+						ft = pick(ph, gb3 + r.pdst, ft);
+						fs = pick(ph, sl, fs);
 					}
+					if (can_hit(pfm, M_SRC)) {
+						uint32_t sl;
+						const uint32_t f = port_probe(s_ports, ptab, pdisp, r.psrc, sl);
+						const uint32_t mk = M_SRC | pm;
+						const bool h = !ph & (r.l4proto != 0) & ((f & mk) == mk) & can_hit(pfm, mk);
+						ft = pick(h, gb3 + r.psrc, ft);
+						fs = pick(h, sl, fs);
+						ph |= h;
+					}
+					fa = pick(ph, HIT, fa);
 				}
 			}
-			q_act = !valid ? A_NONE : r.defer ? A_DEFER : fa;
-			q_tag = valid && !r.defer ? ft : CT_NONE;
-			q_len = len;
+			PMARK("B");
+			q_pk = pk3(pick(!valid, A_NONE, pick(r.defer, A_DEFER, fa)),
+				   pick(valid & !r.defer, fs, XFG_PORT_TAB), len);
+			q_tag = pick(valid & !r.defer, ft, CT_NONE);
 			q_wa = q_wb = ~0u;
 			if ((q_f & (KF_A | KF_AZ)) == KF_A && !(dg & 4))
 				q_wa = gload32(bl + 4ull * xfg_bloom_word(q_ha, bw));
@@ -978,23 +1077,38 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 				q_wb = gload32(bl + 4ull * xfg_bloom_word(q_hb, bw));
 		}
 
-		// ---- L: tile k-1's candidate bucket lines
-		if (lsel && !(dg & 2)) {
-			const uint64_t lp = bk + (uint64_t)r_b * XFG_BUCKET_BYTES;
-			r_line.q0 = gload128(lp);
-			r_line.q1 = gload128(lp + 16);
-			r_line.q2 = gload128(lp + 32);
-			r_line.q3 = gload128(lp + 48);
+		PMARK("L");
+		// ---- L: tile k-1's candidate bucket lines, LDS-DMA'd into the
+		// wave's rows (free again once P has read them): instruction q
+		// carries packets 16q..16q+15, four lanes a line, so every line is
+		// one full 64-byte request
+		{
+			const unsigned long long need = __ballot(lsel && !(dg & 2));
+			if (need) {
+				__builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): P's row reads are done
+				__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+				for (int q = 0; q < 4; q++) {
+					const uint32_t p = q * 16 + (lane >> 2);
+					const uint32_t pj = lane & 3;
+					const uint32_t bp = __shfl(r_b, (int)p);
+					if ((need >> p) & 1)
+						__builtin_amdgcn_global_load_lds(
+							(const __attribute__((address_space(1))) void *)(
+								bk + (uint64_t)bp * XFG_BUCKET_BYTES + pj * 16),
+							(__attribute__((address_space(3))) void *)(rows + q * 256), 16, 0, 0);
+				}
+			}
 		}
+		PMARK("I");
 		// ---- tile k+2's windows, last: in flight for two iterations
 		__builtin_amdgcn_sched_barrier(0);
 		issue(tP + 2 * step, cur, curlen);
 		__builtin_amdgcn_sched_barrier(0);
-		return true;
 	};
 
 	u32x4 preA[CPP], preB[CPP];
-	uint32_t lenA[2] = { 0, 0 }, lenB[2] = { 0, 0 };
+	uint16_t lenA[2] = { 0, 0 }, lenB[2] = { 0, 0 };
 	// (scheduling barriers keep the issue order the waits count on)
 	if (nt) {
 		issue(first, preA, lenA);
@@ -1002,12 +1116,14 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 		issue(first + step, preB, lenB);
 		__builtin_amdgcn_sched_barrier(0);
 	}
-	for (uint32_t k = 0;; k += 2) {
-		if (!iteration(k, preA, lenA))
-			break;
-		if (!iteration(k + 1, preB, lenB))
-			break;
+	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 3 : 0u;
+	uint32_t k = 0;
+	for (; k + 1 < iters; k += 2) {
+		iteration(k, preA, lenA);
+		iteration(k + 1, preB, lenB);
 	}
+	if (k < iters)
+		iteration(k, preA, lenA);
 
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
 		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
@@ -1017,19 +1133,21 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 			act = classify_one<FEAT>(a, s_ports, gi, len, tag);
 			__builtin_nontemporal_store((uint8_t)act, a.verdicts + gi);
 		}
-		count(tag);
+		count(tag, XFG_PORT_TAB);
 		stat(act, len);
 	}
 
-	const unsigned long long v[6] = { st_c0, st_b0, st_c1, st_b1, st_c2, st_b2 };
+	const uint32_t vb[3] = { st_b0, st_b1, st_b2 }, vc[3] = { st_c0, st_c1, st_c2 };
 #pragma unroll
-	for (int kk = 0; kk < 6; kk++) {
-		unsigned long long x = v[kk];
+	for (int kk = 0; kk < 3; kk++) {
+		unsigned long long x = vb[kk];
 #pragma unroll
 		for (int o = 32; o > 0; o >>= 1)
 			x += __shfl_xor(x, o);
-		if (lane == 0 && x)
-			atomicAdd(&s_stats[kk], x);
+		if (lane == 0 && vc[kk]) {
+			atomicAdd(&s_stats[2 * kk], (unsigned long long)vc[kk]);
+			atomicAdd(&s_stats[2 * kk + 1], x);
+		}
 	}
 	if (lane == 0)
 		s_tn[wv] = tn;
@@ -1037,8 +1155,14 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
 	cn.flush(a, tid, NT);
-	if (a.tlog)   // (win is free now: the partition scratch)
-		log_partition<NW>(a, s_tn, win, win + XFG_LOG_PARTS, tid, NT);
+	if constexpr (PORTS)
+		if (ptab)
+			for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
+				if (s_pcnt[i])
+					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
+	static_assert(NW * 64 * ROWDW >= 4 * XFG_LOG_PARTS + LOG_CHUNK, "partition scratch");
+	if (a.tlog && !(dg & 16))   // (win is free now: the partition scratch)
+		log_partition<NW>(a, s_tn, win, tid);
 }
 
 }  // namespace
