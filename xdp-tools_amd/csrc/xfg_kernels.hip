@@ -845,16 +845,17 @@ __device__ __forceinline__ void log_append(uint32_t *region, uint32_t &cnt, uint
 }
 
 // Workgroup end: the NW wave regions (counts in s_n) into the partition
-// buffers.  Two passes over the regions: an LDS histogram, one reservation
+// buffers.  s_hist: the workgroup's per-partition entry counts (LDS; built
+// during the loop by the appenders, or here when null).  One reservation
 // per partition in its buffer (pfill), then chunks of LOG_CHUNK entries
 // counting-sorted by partition in LDS and written out as per-partition runs
 // (consecutive lanes, consecutive addresses).  s: LDS scratch of
 // 4 * XFG_LOG_PARTS + LOG_CHUNK words.  Whole workgroup, after a barrier.
-constexpr uint32_t LOG_CHUNK = 2048;
+constexpr uint32_t LOG_CHUNK = 4096;
 
 template <int NW>
-__device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t *s_n, uint32_t *s,
-					      int tid)
+__device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t *s_n,
+					      const uint32_t *s_hist, uint32_t *s, int tid)
 {
 	constexpr int NTH = 64 * NW, K = LOG_CHUNK / NTH;
 	static_assert(LOG_CHUNK % NTH == 0, "chunk: whole entries per thread");
@@ -869,15 +870,17 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 		s_h[i] = 0;
 		s_cur[i] = 0;
 	}
-	__syncthreads();
-	for (int w = 0; w < NW; w++) {
-		const uint32_t *reg = a.tlog + r0 + (uint64_t)w * a.defer_cap;
-		for (uint32_t e = tid; e < s_n[w]; e += nthr)
-			atomicAdd(&s_h[log_part(reg[e])], 1u);
+	if (!s_hist) {
+		__syncthreads();
+		for (int w = 0; w < NW; w++) {
+			const uint32_t *reg = a.tlog + r0 + (uint64_t)w * a.defer_cap;
+			for (uint32_t e = tid; e < s_n[w]; e += nthr)
+				atomicAdd(&s_h[log_part(reg[e])], 1u);
+		}
 	}
 	__syncthreads();
 	for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
-		const uint32_t c = s_h[p];
+		const uint32_t c = s_hist ? s_hist[p] : s_h[p];
 		s_b[p] = c ? atomicAdd(&a.pfill[p], c) : 0;
 		s_h[p] = 0;
 	}
@@ -984,6 +987,39 @@ __device__ __forceinline__ uint32_t classify_one(const xfg_kargs &a, const uint3
 	Pkt<0> p{ nullptr, pkt_ptr(a, gi), len };
 	const Parsed r = parse<FEAT, 0>(p);
 	return lookups<FEAT, false>(a, LazyKeys<Pkt<0>>{ p }, r, s_ports, tag);
+}
+
+// A deferred packet of the pipelined kernels (fixed stride >= W, no
+// offsets or descriptors): its first W bytes staged into the lane's LDS row
+// with CPP independent 16-byte loads (one round trip), then the reference
+// program over that window (bytes past it from HBM, rare) -- instead of a
+// chain of dependent byte loads.  Whole wave; lanes with ok false idle.
+template <uint32_t FEAT, int W>
+__device__ __forceinline__ uint32_t classify_staged(const xfg_kargs &a, const uint32_t *s_ports,
+						    uint32_t *row, bool ok, uint64_t gi, uint32_t len,
+						    uint32_t &tag)
+{
+	constexpr int CPP = W / 16;
+	const uint8_t *g = a.data + gi * (uint64_t)a.stride;
+	u32x4 v[CPP];
+#pragma unroll
+	for (int it = 0; it < CPP; it++)
+		v[it] = ok ? reinterpret_cast<const u32x4 *>(g)[it] : u32x4{ 0, 0, 0, 0 };
+	__builtin_amdgcn_wave_barrier();
+#pragma unroll
+	for (int it = 0; it < CPP; it++) {
+		row[4 * it] = v[it].x;
+		row[4 * it + 1] = v[it].y;
+		row[4 * it + 2] = v[it].z;
+		row[4 * it + 3] = v[it].w;
+	}
+	__builtin_amdgcn_wave_barrier();
+	tag = CT_NONE;
+	if (!ok)
+		return A_NONE;
+	Pkt<W> p{ row, g, len };
+	const Parsed r = parse<FEAT, W>(p);
+	return lookups<FEAT, false>(a, LazyKeys<Pkt<W>>{ p }, r, s_ports, tag);
 }
 
 // Stage the ruled ports into LDS: the table into s_tab (static), or the

@@ -684,7 +684,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 	cn.flush(a, tid, NT);
 	static_assert(NW * 64 * ROWDW >= 4 * XFG_LOG_PARTS + LOG_CHUNK, "partition scratch");
 	if (a.tlog)   // (win is free now: the partition scratch)
-		log_partition<NW>(a, s_tn, win, tid);
+		log_partition<NW>(a, s_tn, nullptr, win, tid);
 }
 
 }  // namespace
@@ -805,6 +805,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
 	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB : 1];   // per port-table slot
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
+	__shared__ uint32_t s_lh[XFG_LOG_PARTS];   // hit-log entries per partition
 	__shared__ unsigned long long s_stats[6];
 	extern __shared__ uint32_t s_dyn[];
 
@@ -838,6 +839,8 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	if constexpr (PORTS)
 		for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
 			s_pcnt[i] = 0;
+	for (int i = tid; i < (int)XFG_LOG_PARTS; i += NT)
+		s_lh[i] = 0;
 	__syncthreads();
 
 	uint32_t *const rows = win + wv * 64 * ROWDW;
@@ -857,6 +860,8 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 		const bool dc = tag < lg_lo;
 		const bool lg = (tag >= lg_lo) & (tag < lg_hi);
 		log_append(tregion, tn, pick(lg, tag, CT_NONE), lane);
+		if (lg)
+			atomicAdd(&s_lh[log_part(tag)], 1u);
 		if constexpr (PORTS)
 			if (ps)
 				atomicAdd(&s_pcnt[pslot], 1u);
@@ -1127,12 +1132,19 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
 		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
-		if (d0 + lane < ndef) {
-			const uint32_t gi = dlist[d0 + lane];
+		const bool ok = d0 + lane < ndef;
+		const uint32_t gi = ok ? dlist[d0 + lane] : 0u;
+		if (ok)
 			len = min(load_len(a, gi), a.stride);
-			act = classify_one<FEAT>(a, s_ports, gi, len, tag);
+#ifdef XFG_DIAG
+		if (dg & 32) {   // diagnostics: the byte-load path
+			if (ok)
+				act = classify_one<FEAT>(a, s_ports, gi, len, tag);
+		} else
+#endif
+			act = classify_staged<FEAT, W>(a, s_ports, const_cast<uint32_t *>(myrow), ok, gi, len, tag);
+		if (ok)
 			__builtin_nontemporal_store((uint8_t)act, a.verdicts + gi);
-		}
 		count(tag, XFG_PORT_TAB);
 		stat(act, len);
 	}
@@ -1162,7 +1174,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
 	static_assert(NW * 64 * ROWDW >= 4 * XFG_LOG_PARTS + LOG_CHUNK, "partition scratch");
 	if (a.tlog && !(dg & 16))   // (win is free now: the partition scratch)
-		log_partition<NW>(a, s_tn, win, tid);
+		log_partition<NW>(a, s_tn, s_lh, win, tid);
 }
 
 }  // namespace
