@@ -203,6 +203,55 @@ def test_cli_ports_traffic(G, cli, tmp_path, policy):
     cli("unload", "veth0")
 
 
+REMOVALS = [("-m src", "dst,tcp,udp"), ("-m dst", "src,tcp,udp"), ("-p udp", "src,dst,tcp"),
+            ("-p tcp", "src,dst,udp"), ("-m src -p udp", "dst,tcp"), ("-m src -p tcp", "dst,udp"),
+            ("-m dst -p udp", "src,tcp"), ("-m dst -p tcp", "src,udp"), ("", ""),
+            ("-m src,dst", ""), ("-p tcp,udp", ""), ("-m src,dst -p tcp,udp", "")]
+
+
+@pytest.mark.parametrize("opts,left", REMOVALS)
+def test_cli_removal_algebra_traffic(G, cli, tmp_path, opts, left):
+    """test-xdp-filter.sh:309-351 (check_port_removal_from_all,
+    test_output_remove): port 54321 with src,dst,tcp,udp, then one removal;
+    the flags `status` prints must be what the HIP path then matches: tcp and
+    udp frames with 54321 as source and as destination port, the verdicts,
+    and the hit count beside the flags."""
+    port = 54321
+
+    def frame(proto, sport, dport):
+        eth = bytes.fromhex("020000000001020000000002" "0800")
+        l4 = sport.to_bytes(2, "big") + dport.to_bytes(2, "big") + (
+            bytes(8) + bytes([0x50, 0x02]) + bytes(6) if proto == 6 else bytes([0, 9, 0, 0]) + b"x")
+        ip = bytes([0x45, 0]) + (20 + len(l4)).to_bytes(2, "big") + bytes(4) + \
+            bytes([64, proto, 0, 0]) + bytes([192, 0, 2, 1, 192, 0, 2, 2])
+        return eth + ip + l4
+    cases = [(6, port, 9), (6, 9, port), (17, port, 9), (17, 9, port)]
+    frames = [frame(*c) for c in cases]
+    pcap = tmp_path / "r.pcap"
+    P.write_pcap(pcap, frames)
+    cli("load", "veth0", "-p", "deny", "-f", "udp,tcp")
+    cli("port", port, "-p", "tcp,udp", "-m", "src,dst")
+    cli("port", port, *opts.split(), "-r")
+    st, _ = _parse_status(cli("status").stdout)
+    if left:
+        assert st[str(port)] == (left, 0)
+    else:
+        assert str(port) not in st
+    fl = set(left.split(",")) if left else set()
+    want = []
+    for proto, sport, dport in cases:
+        pr = "tcp" if proto == 6 else "udp"
+        hit = pr in fl and (("dst" in fl and dport == port) or ("src" in fl and sport == port))
+        want.append(2 if hit else 1)   # deny policy: a hit passes
+    cli("run", "veth0", pcap, "-d", tmp_path / "v.pcapng", "-q")
+    assert [g[2] for g in P.read_verdict_pcapng(tmp_path / "v.pcapng")] == want
+    st, stats = _parse_status(cli("status").stdout)
+    if left:
+        assert st[str(port)] == (left, want.count(2))
+    assert stats["XDP_PASS"] == want.count(2) and stats["XDP_DROP"] == want.count(1)
+    cli("unload", "veth0")
+
+
 @pytest.mark.parametrize("n", [0, 1, 15, 4095, 4096, 4097, 65536 * 3 + 7, (1 << 22) + 13])
 def test_compact_matches_nonzero(G, n):
     """Ordered verdict compaction (xfg_compact) equals np.nonzero for every

@@ -111,7 +111,10 @@ def rand_keys(seed: int, n: int, keylen: int, distinct: bool = True) -> np.ndarr
     if n:
         synth().xfs_rand_keys(seed, n, keylen, ptr(out))
     if distinct and n:
-        _, idx = np.unique(out, axis=0, return_index=True)
+        # first occurrence of each key (a flat view sorts far faster than axis=0)
+        flat = (out.view("<u4").ravel() if keylen == 4 else
+                out.view(np.dtype((np.void, keylen))).ravel())
+        _, idx = np.unique(flat, return_index=True)
         out = out[np.sort(idx)]
     return out
 

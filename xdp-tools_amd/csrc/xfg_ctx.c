@@ -1587,24 +1587,49 @@ int xfg_comm_unique_id(uint8_t id[XFG_COMM_ID_BYTES])
 	return 0;
 }
 
+/* The reduction copies (red_*) and the communicator.  A second init
+ * replaces both; a failed init leaves the context without either. */
+static void comm_release(xfg_ctx *ctx)
+{
+	struct xfg_dev *d = &ctx->dev[0];
+	if (ctx->comm_ready) {
+		ncclCommDestroy(ctx->comm);
+		ctx->comm_ready = 0;
+	}
+	ctx->reduced = 0;
+	hipSetDevice(d->ordinal);
+	for (int i = 0; i < NMAPS_HASH; i++) {
+		hipFree(d->m[i].red_hits);
+		d->m[i].red_hits = NULL;
+	}
+	hipFree(d->red_port_hits);
+	d->red_port_hits = NULL;
+	hipFree(d->red_stats);
+	d->red_stats = NULL;
+}
+
 int xfg_comm_init(xfg_ctx *ctx, int nranks, int rank, const uint8_t id[XFG_COMM_ID_BYTES])
 {
 	int err = 0;
 	ncclUniqueId u;
-	if (!ctx || ctx->ndev != 1 || nranks < 1 || rank < 0 || rank >= nranks)
+	if (!ctx || !id || ctx->ndev != 1 || nranks < 1 || rank < 0 || rank >= nranks)
 		return -EINVAL;
 	struct xfg_dev *d = &ctx->dev[0];
 	memcpy(&u, id, sizeof(u));
+	comm_release(ctx);
 	HIPCHK(hipSetDevice(d->ordinal));
 	for (int i = 0; i < NMAPS_HASH; i++)
 		HIPCHK(hipMalloc((void **)&d->m[i].red_hits, ((size_t)ctx->t[i].nslots + 1) * 8));
 	HIPCHK(hipMalloc((void **)&d->red_port_hits, XFG_PORT_MAP_ENTRIES * 8));
 	HIPCHK(hipMalloc((void **)&d->red_stats, 10 * 8));
-	if (ncclCommInitRank(&ctx->comm, nranks, u, rank) != ncclSuccess)
-		return -EIO;
+	if (ncclCommInitRank(&ctx->comm, nranks, u, rank) != ncclSuccess) {
+		err = -EIO;
+		goto fail;
+	}
 	ctx->comm_ready = 1;
 	return 0;
 fail:
+	comm_release(ctx);
 	return err;
 }
 
@@ -1616,15 +1641,21 @@ int xfg_comm_allreduce(xfg_ctx *ctx)
 	struct xfg_dev *d = &ctx->dev[0];
 	HIPCHK(hipSetDevice(d->ordinal));
 	HIPCHK(hipStreamSynchronize(d->stream));
+	ctx->reduced = 0;
 	if (ncclGroupStart() != ncclSuccess)
 		return -EIO;
-	for (int i = 0; i < NMAPS_HASH; i++)
-		ncclAllReduce(d->m[i].hits, d->m[i].red_hits, (size_t)ctx->t[i].nslots + 1,
-			      ncclUint64, ncclSum, ctx->comm, d->stream);
-	ncclAllReduce(d->port_hits, d->red_port_hits, XFG_PORT_MAP_ENTRIES, ncclUint64, ncclSum,
-		      ctx->comm, d->stream);
-	ncclAllReduce(d->stats, d->red_stats, 10, ncclUint64, ncclSum, ctx->comm, d->stream);
-	if (ncclGroupEnd() != ncclSuccess)
+	ncclResult_t r = ncclSuccess;
+	for (int i = 0; i < NMAPS_HASH && r == ncclSuccess; i++)
+		r = ncclAllReduce(d->m[i].hits, d->m[i].red_hits, (size_t)ctx->t[i].nslots + 1,
+				  ncclUint64, ncclSum, ctx->comm, d->stream);
+	if (r == ncclSuccess)
+		r = ncclAllReduce(d->port_hits, d->red_port_hits, XFG_PORT_MAP_ENTRIES, ncclUint64,
+				  ncclSum, ctx->comm, d->stream);
+	if (r == ncclSuccess)
+		r = ncclAllReduce(d->stats, d->red_stats, 10, ncclUint64, ncclSum, ctx->comm, d->stream);
+	/* the group is closed whatever happened inside it */
+	const ncclResult_t e = ncclGroupEnd();
+	if (r != ncclSuccess || e != ncclSuccess)
 		return -EIO;
 	HIPCHK(hipStreamSynchronize(d->stream));
 	ctx->reduced = 1;
