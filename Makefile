@@ -3,7 +3,8 @@
 #   xdp-tools_amd/bin/xdp-filter          the CLI over the C ABI
 #   tools/libxfsynth.so                    synthetic traffic (tests / bench)
 #   oracle/build/liboracle.so              CPU restatement (tests / bench cpu_baseline)
-# `make ref` additionally builds oracle/_ref/ from /root/reference (container only).
+# `make asan` builds the host C (restatement, runtime, I/O, CLI) under ASAN +
+# UBSAN for the CPU suite's sanitizer run (tools/asan_suite.sh).
 JOBS ?= 8
 
 all: product synth oracle diag
@@ -22,12 +23,16 @@ tools/libxfsynth.so: tools/xfsynth.c
 oracle:
 	$(MAKE) -C oracle
 
-ref:
-	$(MAKE) -C oracle ref
+asan: product
+	$(MAKE) -C oracle asan
+	$(MAKE) -C xdp-tools_amd asan
+	@mkdir -p tools/build-asan
+	gcc -O1 -g -fPIC -Wall -fsanitize=address,undefined -fno-omit-frame-pointer \
+		-fno-sanitize-recover=undefined -shared -o tools/build-asan/libxfsynth.so tools/xfsynth.c
 
 clean:
 	$(MAKE) -C xdp-tools_amd clean
 	$(MAKE) -C oracle clean
-	rm -f tools/libxfsynth.so
+	rm -rf tools/libxfsynth.so tools/build-asan
 
-.PHONY: all product synth oracle ref diag clean
+.PHONY: all product synth oracle diag asan clean

@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/xdpfilter_golden.npz from the UNMODIFIED reference.
+"""Generate tests/golden/xdpfilter_golden.npz: the regression fixture.
 
-Runs the ten reference programs (xdp-filter/xdpfilt_*.c compiled as host C by
-oracle/Makefile into oracle/_ref/, container only) over:
+Runs the ten programs of the CPU restatement (oracle/xf_oracle.c) over:
   * every known-answer frame of tests/kat.py (SURVEY.md Appendix A and the
     behaviours of xdp-filter/tests/test-xdp-filter.sh / test_basic.py) with
     the rule set kat_rules();
   * a seeded structured-fuzz corpus (tools/xfsynth.c) with a random rule set;
 and stores inputs + expected outputs (verdicts, rule values after the run,
 per-action stats) as plain arrays.  The fixture is data only; regenerate with
-`make ref && python tests/golden/make_golden.py`.
+`make oracle && python tests/golden/make_golden.py`.
+
+Provenance: round 1 generated these same arrays from the reference's
+xdpfilt_*.c compiled for the host against stand-in BPF headers; such a build
+is not a reference build by this project's rules (the reference needs
+libbpf's headers and the kernel's map runtime, absent here: DESIGN.md §2),
+so it was removed and the fixture is now what the restatement produces --
+byte-identical to the round-1 file.  It pins regressions of the restatement
+and of the HIP path; the reference-held expectations are tests/kat.py's rows.
 """
 import os
 import sys
@@ -47,8 +54,6 @@ def rules_arrays(prefix, rs: X.RuleSet, out):
 
 
 def main():
-    if not X.ref_available():
-        sys.exit("oracle/_ref not built: run `make ref` (needs /root/reference)")
     out = {}
     # ---- known-answer corpus
     kf = kat.kat_frames()
@@ -66,7 +71,7 @@ def main():
 
     for v, feats in X.VARIANTS:
         for tag, data, lens, rs in (("kat", kdata, klens, krules), ("fuzz", fdata, flens, frules)):
-            verd, after, st = X.run_ref(v, data, lens, rs, stride=STRIDE)
+            verd, after, st = X.run_oracle(feats, data, lens, rs, stride=STRIDE)
             p = f"{tag}_{v}_"
             out[p + "verdicts"] = verd
             nz = np.nonzero(rs.ports | after.ports)[0]

@@ -19,7 +19,8 @@ import pytest
 import xfgpu as G
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-XF = os.path.join(ROOT, "xdp-tools_amd", "bin", "xdp-filter")
+XF = os.path.join(ROOT, "xdp-tools_amd",
+                  "bin-asan" if os.environ.get("XFG_LIB") == "asan" else "bin", "xdp-filter")
 
 
 @pytest.fixture

@@ -23,7 +23,8 @@ import xftools as X
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-XF = os.path.join(ROOT, "xdp-tools_amd", "bin", "xdp-filter")
+XF = os.path.join(ROOT, "xdp-tools_amd",
+                  "bin-asan" if os.environ.get("XFG_LIB") == "asan" else "bin", "xdp-filter")
 
 
 @pytest.fixture(scope="module")

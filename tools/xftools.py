@@ -3,11 +3,9 @@
 ctypes bindings for:
   * tools/libxfsynth.so        seeded synthetic traffic (workloads C2..C5, fuzz)
   * oracle/build/liboracle.so  our CPU restatement of the xdpfilt_* program
-  * oracle/_ref/libxfref_*.so  the unmodified reference program compiled as
-                               host C (container-built; travels as a .so)
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use the
-oracle/reference bindings, and only as checkers / the CPU baseline.
+oracle binding, and only as the checker / the CPU baseline.
 """
 from __future__ import annotations
 
@@ -18,6 +16,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# XFG_LIB=asan: the sanitizer builds (make asan; tools/asan_suite.sh)
+_ASAN = os.environ.get("XFG_LIB") == "asan"
 
 FEAT_TCP, FEAT_UDP, FEAT_IPV6, FEAT_IPV4, FEAT_ETHERNET = 1, 2, 4, 8, 16
 FEAT_ALL = 31
@@ -94,7 +94,7 @@ _synth = None
 def synth():
     global _synth
     if _synth is None:
-        lib = C.CDLL(os.path.join(ROOT, "tools", "libxfsynth.so"))
+        lib = C.CDLL(os.path.join(ROOT, "tools", "build-asan" if _ASAN else "", "libxfsynth.so"))
         lib.xfs_gen_workload.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint32,
                                          _u8p, _u32p, _u8p, C.c_uint32, _u8p, C.c_uint32,
                                          _u16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
@@ -185,7 +185,7 @@ _oracle = None
 def oracle():
     global _oracle
     if _oracle is None:
-        lib = C.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so"))
+        lib = C.CDLL(os.path.join(ROOT, "oracle", "build-asan" if _ASAN else "build", "liboracle.so"))
         lib.xfo_map_new.restype = C.c_void_p
         lib.xfo_map_new.argtypes = [C.c_uint32, C.c_uint32, _u8p]
         lib.xfo_map_free.argtypes = [C.c_void_p]
@@ -248,49 +248,3 @@ def run_oracle(features, data, lens, rules: RuleSet, stride=0, offsets=None,
     return verdicts, r, st.reshape(5, 2)
 
 
-# ----------------------------------------------------------------- reference
-_ref = {}
-
-
-def ref_path(variant: str) -> str:
-    short = variant.replace("xdpfilt_", "")
-    return os.path.join(ROOT, "oracle", "_ref", f"libxfref_{short}.so")
-
-
-def ref_available() -> bool:
-    return all(os.path.exists(ref_path(v)) for v, _ in VARIANTS)
-
-
-def ref_lib(variant: str):
-    if variant not in _ref:
-        lib = C.CDLL(ref_path(variant))
-        lib.xfref_name.restype = C.c_char_p
-        lib.xfref_features.restype = C.c_uint32
-        lib.xfref_run.argtypes = [_u8p, _u64p, C.c_uint32, _u32p, C.c_uint64, _u64p,
-                                  C.c_uint32, _u8p, _u64p, C.c_uint32, _u8p, _u64p,
-                                  C.c_uint32, _u8p, _u64p, _u8p, _u64p]
-        _ref[variant] = lib
-    return _ref[variant]
-
-
-def run_ref(variant, data, lens, rules: RuleSet, stride=0, offsets=None, stats=None,
-            in_place=False):
-    """Run the unmodified reference program; returns (verdicts, rules_after, stats[5,2]).
-    in_place: update `rules` (already prepared()) directly, so the driver's
-    key index is reused across calls (timing loops)."""
-    lib = ref_lib(variant)
-    lib.xfref_cache_index(1 if in_place else 0)
-    r = rules if in_place else rules.prepared().copy()
-    n = len(lens)
-    verdicts = np.zeros(n, np.uint8)
-    st = np.zeros(10, np.uint64) if stats is None else stats.reshape(10)
-    lens32 = np.ascontiguousarray(lens, np.uint32)
-    offs = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
-    rc = lib.xfref_run(ptr(data), ptr(offs, _u64p), stride, ptr(lens32, _u32p), n,
-                       ptr(r.ports, _u64p), len(r.v4_vals), ptr(r.v4_keys), ptr(r.v4_vals, _u64p),
-                       len(r.v6_vals), ptr(r.v6_keys), ptr(r.v6_vals, _u64p),
-                       len(r.eth_vals), ptr(r.eth_keys), ptr(r.eth_vals, _u64p),
-                       ptr(verdicts), ptr(st, _u64p))
-    if rc:
-        raise RuntimeError("reference run failed")
-    return verdicts, r, st.reshape(5, 2)

@@ -26,10 +26,12 @@ except Exception:  # torch absent: the library uses /opt/rocm's runtime
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# XFG_LIB=diag selects the diagnostics build (measurement knobs; tools/ only)
-LIB_PATH = os.path.join(os.path.dirname(HERE), "lib",
-                        "libxdpfilter_gpu_diag.so" if os.environ.get("XFG_LIB") == "diag"
-                        else "libxdpfilter_gpu.so")
+# XFG_LIB=diag selects the diagnostics build (measurement knobs; tools/ only),
+# XFG_LIB=asan the sanitizer build of the host C (the CPU suite under
+# tools/asan_suite.sh)
+_LIBS = {"diag": ("lib", "libxdpfilter_gpu_diag.so"), "asan": ("lib-asan", "libxdpfilter_gpu.so")}
+LIB_PATH = os.path.join(os.path.dirname(HERE),
+                        *_LIBS.get(os.environ.get("XFG_LIB", ""), ("lib", "libxdpfilter_gpu.so")))
 
 FEAT_TCP, FEAT_UDP, FEAT_IPV6, FEAT_IPV4, FEAT_ETHERNET = 1, 2, 4, 8, 16
 FEAT_ALL = 31
