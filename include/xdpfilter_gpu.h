@@ -186,12 +186,37 @@ int xfg_classify_descs(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *batch
 		       uint8_t *verdicts, void *stream);
 
 /*
- * Host-resident batch: copies packets to the device (pinned staging,
- * pipelined H2D / kernel / D2H over chunks), classifies, copies verdicts
- * back.  Packet layout as struct xfg_batch but in host memory.
+ * Host-resident batch (struct xfg_batch in host memory): classifies it on
+ * device @dev and writes the verdicts to host memory.  Only each frame's
+ * first 128 bytes (its header window) and its length cross PCIe -- gathered
+ * into pinned staging by a per-device thread pool and pipelined H2D / kernel
+ * / D2H over chunks; a frame whose program reads past its window is sent
+ * again whole and classified from it, so verdicts, counters and stats are
+ * exactly those of a whole-frame run.  A fixed stride of at most 128 bytes
+ * is staged slot for slot.  Concurrent calls on different devices run in
+ * parallel; staging memory per device is fixed (about 70 MB pinned).
+ * Replaces the per-packet program run of the attach path
+ * (xdp-filter/xdpfilt_prog.h:214-310 over frames the kernel hands it).
  */
 int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
 		      uint8_t *verdicts);
+
+/*
+ * AF_XDP RX in host memory: the consumer side of an XDP socket's RX ring
+ * (xsk_ring_cons__peek() / xsk_ring_cons__rx_desc() / xsk_ring_cons__release(),
+ * headers/xdp/xsk.h:80-86,143-165).  Packet i is ring record
+ * descs[(first + i) & mask], a struct xdp_desc {u64 addr; u32 len; u32
+ * options} (headers/linux/if_xdp.h:110-114), over the host UMEM @umem of
+ * @umem_bytes: its bytes start at umem + (addr & ((1 << 48) - 1)) +
+ * (addr >> 48) (xsk_umem__add_offset_to_addr(), headers/xdp/xsk.h:173-186;
+ * unaligned-chunk mode).  mask = ring entries - 1 (a power of two), or
+ * 0xffffffff for a plain array; count <= entries.  Classified as
+ * xfg_classify_host does (header windows, exact whole-frame fallback);
+ * -EINVAL if a frame lies outside the UMEM.  The caller releases the ring
+ * entries after the call returns.
+ */
+int xfg_classify_xsk_host(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *batch,
+			  uint64_t umem_bytes, uint8_t *verdicts);
 
 /*
  * Verdict compaction: writes the indices i (ascending) with verdicts[i] ==

@@ -296,3 +296,104 @@ def test_compact_pass_list_after_classify(G):
     np.testing.assert_array_equal(d_i.download(np.zeros(cnt, np.uint32)),
                                   np.nonzero(ov == 2)[0].astype(np.uint32))
     f.close()
+
+
+def _long_header_frames(rules, n, seed):
+    """IPv6 frames whose L4 header lies past the 128-byte header window
+    (hop-by-hop chains of 16-40 bytes per header before UDP/TCP to a ruled
+    or unruled port), padded to 200-1400 bytes: the host path's fallback."""
+    import pktbuild as PB
+    rng = np.random.default_rng(seed)
+    ruled = [k for k in np.nonzero(rules.prepared().ports)[0]]
+    out = []
+    for i in range(n):
+        chain = b""
+        nx = int(rng.integers(2, 6))
+        for j in range(nx):
+            chain += PB.ext(0 if j + 1 < nx else (17 if i % 2 else 6), int(rng.integers(1, 5)))
+        port = int(ruled[i % len(ruled)]) if ruled and i % 3 else 4242
+        port = ((port & 0xff) << 8) | (port >> 8) if ruled and i % 3 else port
+        l4 = PB.udp(1000 + i, port) if i % 2 else PB.tcp(1000 + i, port)
+        fr = PB.eth(ethertype=0x86DD) + PB.ipv6(nh=0, payload=chain + l4)
+        out.append(fr + bytes(int(rng.integers(0, 1200))))
+    return out
+
+
+@pytest.mark.parametrize("layout", ["stride", "offsets_u16"])
+def test_classify_host_header_windows_exact(G, layout):
+    """xfg_classify_host sends 128-byte header windows; frames whose program
+    reads past the window are classified again whole.  Verdicts, counters and
+    stats equal a whole-frame oracle run, with fallbacks actually taken."""
+    rules, pool = X.random_rules(101, n4=200, n6=100, ne=30, nports=40)
+    fuzz_d, fuzz_l = X.gen_fuzz(31, 30000, 160, rules, pool)
+    frames = P.frames_of(fuzz_d, fuzz_l, stride=160) + _long_header_frames(rules, 3000, 5)
+    rng = np.random.default_rng(8)
+    frames = [frames[i] for i in rng.permutation(len(frames))]
+    feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    if layout == "stride":
+        stride = 1536
+        data = np.zeros(len(frames) * stride, np.uint8)
+        lens = np.array([len(f) for f in frames], np.uint32)
+        for i, fr in enumerate(frames):
+            data[i * stride:i * stride + len(fr)] = np.frombuffer(fr, np.uint8)
+        ov, orules, ost = X.run_oracle(feats, data, lens, rules, stride=stride)
+        offs = None
+    else:
+        data, offs, lens = P.batch_from(frames)
+        lens = lens.astype(np.uint16)
+        stride = 0
+        ov, orules, ost = X.run_oracle(feats, data, lens.astype(np.uint32), rules, offsets=offs)
+    f = G.Filter(feats, ndev=1)
+    f.load_rules(rules)
+    v = f.classify_host(data, lens, stride=stride, offsets=offs)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(f.stats(), ost)
+    r = rules.prepared()
+    np.testing.assert_array_equal(f.values_of(G.MAP_IPV6, r.v6_keys), orules.v6_vals)
+    np.testing.assert_array_equal(f.values_of(G.MAP_PORTS, np.arange(65536, dtype=np.uint32)),
+                                  orules.ports)
+    f.close()
+
+
+def test_classify_xsk_host_ring_wrap_unaligned(G):
+    """The host-memory AF_XDP consumer (xfg_classify_xsk_host): a UMEM of
+    4 KiB chunks in host memory, frames at aligned and unaligned-chunk
+    addresses (offset in bits 48..63, headers/xdp/xsk.h:173-186), an RX ring
+    view that wraps; long-header frames take the whole-frame fallback."""
+    rules, pool = X.random_rules(111, n4=120, n6=60, ne=20, nports=30)
+    fd, fl = X.gen_fuzz(29, 20000, 160, rules, pool)
+    frames = P.frames_of(fd, fl, stride=160) + _long_header_frames(rules, 1500, 9)
+    n = len(frames)
+    data, offs, lens = P.batch_from(frames)
+    feats = X.VARIANT_FEATURES["xdpfilt_alw_all"]
+    ov, orules, ost = X.run_oracle(feats, data, lens, rules, offsets=offs)
+    rng = np.random.default_rng(12)
+    nchunks = n + 64
+    perm = rng.permutation(nchunks)[:n]
+    umem = np.zeros(nchunks * 4096, np.uint8)
+    addr = np.zeros(n, np.uint64)
+    for i, fr in enumerate(frames):
+        base, head = int(perm[i]) * 4096, 256 + 16 * (i % 3)
+        umem[base + head:base + head + len(fr)] = np.frombuffer(fr, np.uint8)
+        addr[i] = (base | (head << 48)) if i % 3 == 2 else base + head
+    ring, first = 32768, 32768 - 1001
+    descs = np.zeros((ring, 2), np.uint64)
+    idx = (first + np.arange(n)) & (ring - 1)
+    descs[idx, 0] = addr
+    descs[idx, 1] = lens.astype(np.uint64)
+    f = G.Filter(feats, ndev=1)
+    f.load_rules(rules)
+    v = f.classify_xsk_host(umem, descs, n, first=first, mask=ring - 1)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(f.stats(), ost)
+    r = rules.prepared()
+    np.testing.assert_array_equal(f.values_of(G.MAP_IPV4, r.v4_keys), orules.v4_vals)
+    np.testing.assert_array_equal(f.values_of(G.MAP_PORTS, np.arange(65536, dtype=np.uint32)),
+                                  orules.ports)
+    with pytest.raises(OSError):      # a frame outside the UMEM
+        bad = descs.copy()
+        bad[idx[0], 0] = umem.nbytes - 8
+        f.classify_xsk_host(umem, bad, n, first=first, mask=ring - 1)
+    with pytest.raises(OSError):      # a ring mask must be 2^k - 1
+        f.classify_xsk_host(umem, descs, n, first=first, mask=1000)
+    f.close()

@@ -70,12 +70,21 @@ struct xfg_dev {
 	 * 2 pipelined IPv4-key mode][window 64, 128][dynamic LDS: none, direct
 	 * counters, port nibble map, both] */
 	int occ[3][2][4];
-	/* host-resident classify: persistent double-buffered staging */
+	/* host-resident classify (xfg_classify_host / xfg_classify_xsk_host),
+	 * under host_lock: a gather pool, two fixed-size staging slots of
+	 * HOST_CH packets x HOST_WIN bytes (header windows, or whole slots of
+	 * a batch with a stride <= HOST_WIN) with their fallback lists, and the
+	 * whole-frame fallback staging (FB_BYTES) */
+	pthread_mutex_t host_lock;
+	struct hpool *pool;
 	uint8_t *hs_hbuf[2], *hs_dbuf[2], *hs_dv[2];
 	uint32_t *hs_hl[2], *hs_dl[2];
+	uint32_t *hs_fb[2], *hs_fbc[2], *hs_hfbc[2];
 	hipStream_t hs_st[2];
 	hipEvent_t hs_done[2];
-	size_t hs_bytes;
+	uint8_t *fb_h, *fb_d, *fb_dv;   /* fallback frames (pinned / device), verdicts */
+	uint64_t *fb_ho, *fb_do;        /* their offsets */
+	uint32_t *fb_hl, *fb_dl, *fb_idx;
 	pthread_mutex_t lock;           /* launch scratch below + compaction scratch */
 	int lock_ok;
 	uint32_t *defer;                /* pipelined kernel: deferred-packet lists */
@@ -90,7 +99,6 @@ struct xfg_dev {
 
 struct xfg_ctx {
 	pthread_mutex_t lock;
-	pthread_mutex_t host_lock;      /* xfg_classify_host: the devices' staging buffers */
 	uint32_t prog_features;
 	const char *prog_name;
 	int ndev;
@@ -182,11 +190,111 @@ static int keylen_of(int map)
 	}
 }
 
+/* ------------------------------------------------------------------ gather pool */
+/* Persistent worker threads of one device's host path: hpool_run(fn, arg)
+ * runs fn(arg, slice, nslices) for every slice, slice 0 on the caller. */
+#define HOST_THREADS 8
+
+struct hpool {
+	pthread_t th[HOST_THREADS];
+	struct hpool_arg {
+		struct hpool *p;
+		int id;
+	} args[HOST_THREADS];
+	int nth;                   /* workers (slices 1..nth) */
+	pthread_mutex_t mu;
+	pthread_cond_t go, done;
+	void (*fn)(void *, int, int);
+	void *arg;
+	unsigned gen;
+	int pending, stop;
+};
+
+static void *hpool_main(void *v)
+{
+	struct hpool_arg *w = v;
+	struct hpool *p = w->p;
+	unsigned seen = 0;
+	pthread_mutex_lock(&p->mu);
+	for (;;) {
+		while (p->gen == seen && !p->stop)
+			pthread_cond_wait(&p->go, &p->mu);
+		if (p->stop)
+			break;
+		seen = p->gen;
+		void (*fn)(void *, int, int) = p->fn;
+		void *arg = p->arg;
+		const int n = p->nth + 1;
+		pthread_mutex_unlock(&p->mu);
+		fn(arg, w->id, n);
+		pthread_mutex_lock(&p->mu);
+		if (--p->pending == 0)
+			pthread_cond_signal(&p->done);
+	}
+	pthread_mutex_unlock(&p->mu);
+	return NULL;
+}
+
+static struct hpool *hpool_start(void)
+{
+	struct hpool *p = calloc(1, sizeof(*p));
+	if (!p)
+		return NULL;
+	pthread_mutex_init(&p->mu, NULL);
+	pthread_cond_init(&p->go, NULL);
+	pthread_cond_init(&p->done, NULL);
+	/* (workers are told their count under the lock, before any run) */
+	pthread_mutex_lock(&p->mu);
+	for (int t = 1; t < HOST_THREADS; t++) {
+		p->args[t] = (struct hpool_arg){ p, t };
+		if (pthread_create(&p->th[t], NULL, hpool_main, &p->args[t]))
+			break;
+		p->nth = t;
+	}
+	pthread_mutex_unlock(&p->mu);
+	return p;
+}
+
+static void hpool_run(struct hpool *p, void (*fn)(void *, int, int), void *arg)
+{
+	pthread_mutex_lock(&p->mu);
+	p->fn = fn;
+	p->arg = arg;
+	p->pending = p->nth;
+	p->gen++;
+	pthread_cond_broadcast(&p->go);
+	pthread_mutex_unlock(&p->mu);
+	fn(arg, 0, p->nth + 1);
+	pthread_mutex_lock(&p->mu);
+	while (p->pending)
+		pthread_cond_wait(&p->done, &p->mu);
+	pthread_mutex_unlock(&p->mu);
+}
+
+static void hpool_stop(struct hpool *p)
+{
+	if (!p)
+		return;
+	pthread_mutex_lock(&p->mu);
+	p->stop = 1;
+	pthread_cond_broadcast(&p->go);
+	pthread_mutex_unlock(&p->mu);
+	for (int t = 1; t <= p->nth; t++)
+		pthread_join(p->th[t], NULL);
+	pthread_cond_destroy(&p->go);
+	pthread_cond_destroy(&p->done);
+	pthread_mutex_destroy(&p->mu);
+	free(p);
+}
+
 /* ------------------------------------------------------------------ open */
 static void dev_free(struct xfg_dev *d)
 {
+	hpool_stop(d->pool);
+	d->pool = NULL;
 	if (d->lock_ok) {
 		pthread_mutex_destroy(&d->lock);
+		pthread_mutex_destroy(&d->host_lock);
 		d->lock_ok = 0;
 	}
 	if (hipSetDevice(d->ordinal) != hipSuccess)
@@ -212,14 +320,25 @@ static void dev_free(struct xfg_dev *d)
 			hipStreamSynchronize(d->hs_st[k]);
 		hipHostFree(d->hs_hbuf[k]);
 		hipHostFree(d->hs_hl[k]);
+		hipHostFree(d->hs_hfbc[k]);
 		hipFree(d->hs_dbuf[k]);
 		hipFree(d->hs_dl[k]);
 		hipFree(d->hs_dv[k]);
+		hipFree(d->hs_fb[k]);
+		hipFree(d->hs_fbc[k]);
 		if (d->hs_done[k])
 			hipEventDestroy(d->hs_done[k]);
 		if (d->hs_st[k])
 			hipStreamDestroy(d->hs_st[k]);
 	}
+	hipHostFree(d->fb_h);
+	hipHostFree(d->fb_ho);
+	hipHostFree(d->fb_hl);
+	hipHostFree(d->fb_idx);
+	hipFree(d->fb_d);
+	hipFree(d->fb_do);
+	hipFree(d->fb_dl);
+	hipFree(d->fb_dv);
 	hipFree(d->defer);
 	hipFree(d->tlog);
 	hipFree(d->pbuf);
@@ -243,6 +362,7 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	hipDeviceProp_t prop;
 
 	pthread_mutex_init(&d->lock, NULL);
+	pthread_mutex_init(&d->host_lock, NULL);
 	d->lock_ok = 1;
 	HIPCHK(hipSetDevice(d->ordinal));
 	HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
@@ -301,7 +421,6 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 	if (!ctx)
 		return -ENOMEM;
 	pthread_mutex_init(&ctx->lock, NULL);
-	pthread_mutex_init(&ctx->host_lock, NULL);
 	err = xfg_select_program(opts->features, &ctx->prog_name, &ctx->prog_features);
 	if (err)
 		goto fail;
@@ -386,7 +505,6 @@ void xfg_close(xfg_ctx *ctx)
 	free(ctx->host_port_vals);
 	free(ctx->port_flags_host);
 	pthread_mutex_destroy(&ctx->lock);
-	pthread_mutex_destroy(&ctx->host_lock);
 	free(ctx);
 }
 
@@ -1297,163 +1415,319 @@ fail:
 	return err;
 }
 
-/* Host-resident batch: pinned double-buffered staging, H2D / kernel / D2H
- * pipelined over two streams.  Whole frames cross PCIe (re-packed at a fixed
- * 16-byte-aligned stride): a verdict may depend on bytes past any fixed
- * header window (long IPv6 extension chains, TCP doff bounds checks against
- * the full length), see DESIGN.md "host-resident rate".  The staging buffers
- * and streams persist in the device (grown on demand), and the repack into
- * pinned memory is split over threads (one memcpy per chunk slice when the
- * batch already has a fixed stride). */
-#define HOST_CH (1u << 18)   /* packets per chunk */
-#define HOST_THREADS 8
+/* Host-resident batches (xfg_classify_host, xfg_classify_xsk_host).
+ *
+ * Only header windows cross PCIe: each packet's first HOST_WIN bytes go to
+ * a pinned staging slot (gathered by the device's thread pool) with its
+ * true length, H2D, and the general kernel classifies them in header-window
+ * mode (kargs.hwin).  A packet whose program would read past its window
+ * (long IPv6 extension chains and the like) is not classified or counted
+ * there: the kernel lists it, and the host sends its whole frame through
+ * the ordinary device path afterwards -- the verdicts, counters and stats
+ * are exactly those of a whole-frame run.  A fixed-stride batch whose
+ * stride is at most HOST_WIN is staged slot for slot instead (one memcpy
+ * per slice; nothing can fall back).  Two staging slots of HOST_CH packets
+ * alternate (gather / H2D / kernel / D2H over two streams); their size is
+ * fixed (HOST_CH x HOST_WIN bytes each), whatever the frames' lengths.
+ * One lock per device: the devices' host paths run concurrently. */
+#define HOST_CH (1u << 18)     /* packets per staging slot */
+#define HOST_WIN 128u          /* header window (bytes) */
+#define FB_BYTES (64u << 20)   /* whole-frame fallback staging */
+#define FB_PKTS (1u << 16)     /* ... and its packets per pass */
 
-struct repack_job {
-	const struct xfg_batch *b;
-	uint8_t *dst;
-	uint32_t *dl;
-	uint64_t first, m;       /* packets [first, first + m) of the batch */
-	uint32_t stride;         /* staging stride */
-	int contiguous;          /* batch stride == staging stride, no offsets */
+/* where packet i of a host batch lies */
+struct hsrc {
+	const uint8_t *data;       /* batch data, or the UMEM */
+	const uint64_t *offsets;
+	uint32_t stride;
+	const void *lens;
+	int lens_u16;
+	const uint64_t *descs;     /* AF_XDP RX ring (xdp_desc records), or NULL */
+	uint32_t first, mask;
 };
 
-static void *repack_run(void *arg)
+static inline const uint8_t *hsrc_ptr(const struct hsrc *s, uint64_t i)
 {
-	struct repack_job *j = arg;
-	const struct xfg_batch *b = j->b;
-	if (j->contiguous) {
-		memcpy(j->dst, (const uint8_t *)b->data + j->first * (uint64_t)j->stride,
-		       j->m * (uint64_t)j->stride);
+	if (s->descs) {
+		/* xsk_umem__add_offset_to_addr(): unaligned-chunk offset in
+		 * bits 48..63 (headers/xdp/xsk.h:173-186) */
+		const uint64_t a = s->descs[2ull * ((s->first + (uint32_t)i) & s->mask)];
+		return s->data + (a & ((1ull << 48) - 1)) + (a >> 48);
 	}
-	for (uint64_t i = 0; i < j->m; i++) {
-		uint64_t gi = j->first + i;
-		uint32_t l = b->lens_u16 ? ((const uint16_t *)b->lens)[gi]
-					 : ((const uint32_t *)b->lens)[gi];
-		if (!j->contiguous) {
-			const uint8_t *src = (const uint8_t *)b->data +
-					     (b->offsets ? b->offsets[gi] : gi * (uint64_t)b->stride);
-			memcpy(j->dst + i * (uint64_t)j->stride, src, l);
-		}
+	return s->data + (s->offsets ? s->offsets[i] : i * (uint64_t)s->stride);
+}
+
+static inline uint32_t hsrc_len(const struct hsrc *s, uint64_t i)
+{
+	if (s->descs)   /* xdp_desc.len: the low half of the record's second word */
+		return (uint32_t)s->descs[2ull * ((s->first + (uint32_t)i) & s->mask) + 1];
+	return s->lens_u16 ? ((const uint16_t *)s->lens)[i] : ((const uint32_t *)s->lens)[i];
+}
+
+struct gather_job {
+	const struct hsrc *src;
+	uint64_t first, m;         /* packets [first, first + m) */
+	uint8_t *dst;
+	uint32_t *dl;
+	uint32_t stride;           /* staging stride: HOST_WIN, or the batch's */
+	int whole;                 /* whole slots (stride <= HOST_WIN, no offsets) */
+};
+
+static void gather_slice(void *arg, int t, int nt)
+{
+	const struct gather_job *j = arg;
+	const uint64_t per = (j->m + nt - 1) / nt;
+	const uint64_t s0 = t * per, s1 = s0 + per < j->m ? s0 + per : j->m;
+	if (s0 >= s1)
+		return;
+	if (j->whole)
+		memcpy(j->dst + s0 * j->stride, j->src->data + (j->first + s0) * j->stride,
+		       (s1 - s0) * j->stride);
+	for (uint64_t i = s0; i < s1; i++) {
+		const uint32_t l = hsrc_len(j->src, j->first + i);
+		if (!j->whole)
+			memcpy(j->dst + i * HOST_WIN, hsrc_ptr(j->src, j->first + i),
+			       l < HOST_WIN ? l : HOST_WIN);
 		j->dl[i] = l;
 	}
-	return NULL;
 }
 
-/* m packets from `first` into staging: HOST_THREADS slices in parallel */
-static void repack(const struct xfg_batch *b, uint8_t *dst, uint32_t *dl, uint64_t first,
-		   uint64_t m, uint32_t stride, int contiguous)
-{
-	struct repack_job jobs[HOST_THREADS];
-	pthread_t th[HOST_THREADS];
-	int started[HOST_THREADS] = { 0 };
-	uint64_t per = (m + HOST_THREADS - 1) / HOST_THREADS;
-	for (int t = 0; t < HOST_THREADS; t++) {
-		uint64_t s0 = t * per, s1 = s0 + per < m ? s0 + per : m;
-		jobs[t] = (struct repack_job){ b, dst + s0 * (uint64_t)stride, dl + s0, first + s0,
-					       s1 > s0 ? s1 - s0 : 0, stride, contiguous };
-		if (t && jobs[t].m && m >= 4096)
-			started[t] = !pthread_create(&th[t], NULL, repack_run, &jobs[t]);
-	}
-	for (int t = HOST_THREADS - 1; t >= 0; t--) {   /* the ones not handed off, here */
-		if (!started[t] && jobs[t].m && (t == 0 || m < 4096 || !started[t]))
-			repack_run(&jobs[t]);
-	}
-	for (int t = 1; t < HOST_THREADS; t++)
-		if (started[t])
-			pthread_join(th[t], NULL);
-}
-
-static int host_staging(struct xfg_dev *d, size_t chunk_bytes)
+static int host_staging(struct xfg_dev *d)
 {
 	int err = 0;
-	if (!d->hs_st[0]) {
-		for (int k = 0; k < 2; k++) {
-			HIPCHK(hipStreamCreateWithFlags(&d->hs_st[k], hipStreamNonBlocking));
-			HIPCHK(hipEventCreate(&d->hs_done[k]));
-			HIPCHK(hipHostMalloc((void **)&d->hs_hl[k], HOST_CH * 4, hipHostMallocDefault));
-			HIPCHK(hipMalloc((void **)&d->hs_dl[k], HOST_CH * 4));
-			HIPCHK(hipMalloc((void **)&d->hs_dv[k], HOST_CH));
-		}
+	if (!d->pool && !(d->pool = hpool_start()))
+		return -ENOMEM;
+	if (d->hs_st[0])
+		return 0;
+	for (int k = 0; k < 2; k++) {
+		HIPCHK(hipStreamCreateWithFlags(&d->hs_st[k], hipStreamNonBlocking));
+		HIPCHK(hipEventCreate(&d->hs_done[k]));
+		HIPCHK(hipHostMalloc((void **)&d->hs_hbuf[k], (size_t)HOST_CH * HOST_WIN,
+				     hipHostMallocDefault));
+		HIPCHK(hipHostMalloc((void **)&d->hs_hl[k], HOST_CH * 4, hipHostMallocDefault));
+		HIPCHK(hipHostMalloc((void **)&d->hs_hfbc[k], 4, hipHostMallocDefault));
+		HIPCHK(hipMalloc((void **)&d->hs_dbuf[k], (size_t)HOST_CH * HOST_WIN));
+		HIPCHK(hipMalloc((void **)&d->hs_dl[k], HOST_CH * 4));
+		HIPCHK(hipMalloc((void **)&d->hs_dv[k], HOST_CH));
+		HIPCHK(hipMalloc((void **)&d->hs_fb[k], HOST_CH * 4));
+		HIPCHK(hipMalloc((void **)&d->hs_fbc[k], 4));
 	}
-	if (chunk_bytes > d->hs_bytes) {
-		for (int k = 0; k < 2; k++) {
-			hipHostFree(d->hs_hbuf[k]);
-			hipFree(d->hs_dbuf[k]);
-			d->hs_hbuf[k] = NULL;
-			d->hs_dbuf[k] = NULL;
+	return 0;
+fail:
+	for (int k = 0; k < 2; k++) {   /* all or nothing: a later call starts over */
+		if (d->hs_st[k])
+			hipStreamDestroy(d->hs_st[k]);
+		if (d->hs_done[k])
+			hipEventDestroy(d->hs_done[k]);
+		hipHostFree(d->hs_hbuf[k]);
+		hipHostFree(d->hs_hl[k]);
+		hipHostFree(d->hs_hfbc[k]);
+		hipFree(d->hs_dbuf[k]);
+		hipFree(d->hs_dl[k]);
+		hipFree(d->hs_dv[k]);
+		hipFree(d->hs_fb[k]);
+		hipFree(d->hs_fbc[k]);
+		d->hs_st[k] = NULL;
+		d->hs_done[k] = NULL;
+		d->hs_hbuf[k] = d->hs_dbuf[k] = d->hs_dv[k] = NULL;
+		d->hs_hl[k] = d->hs_dl[k] = d->hs_fb[k] = d->hs_fbc[k] = d->hs_hfbc[k] = NULL;
+	}
+	return err;
+}
+
+static int fb_staging(struct xfg_dev *d)
+{
+	int err = 0;
+	if (d->fb_h)
+		return 0;
+	HIPCHK(hipHostMalloc((void **)&d->fb_ho, FB_PKTS * 8, hipHostMallocDefault));
+	HIPCHK(hipHostMalloc((void **)&d->fb_hl, FB_PKTS * 4, hipHostMallocDefault));
+	HIPCHK(hipHostMalloc((void **)&d->fb_idx, (size_t)HOST_CH * 4, hipHostMallocDefault));
+	HIPCHK(hipMalloc((void **)&d->fb_d, FB_BYTES + 64));
+	HIPCHK(hipMalloc((void **)&d->fb_do, FB_PKTS * 8));
+	HIPCHK(hipMalloc((void **)&d->fb_dl, FB_PKTS * 4));
+	HIPCHK(hipMalloc((void **)&d->fb_dv, FB_PKTS));
+	HIPCHK(hipHostMalloc((void **)&d->fb_h, FB_BYTES + 64, hipHostMallocDefault));
+	return 0;
+fail:
+	hipHostFree(d->fb_ho);
+	hipHostFree(d->fb_hl);
+	hipHostFree(d->fb_idx);
+	hipFree(d->fb_d);
+	hipFree(d->fb_do);
+	hipFree(d->fb_dl);
+	hipFree(d->fb_dv);
+	d->fb_ho = NULL;
+	d->fb_hl = d->fb_idx = d->fb_dl = NULL;
+	d->fb_d = d->fb_dv = NULL;
+	d->fb_do = NULL;
+	return err;
+}
+
+/* Classify a device-resident sub-batch on stream st (kernels on the device
+ * stream, ordered after st's uploads; st after the kernels). */
+static int host_launch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *sub,
+		       uint8_t *dv, int hwin, uint32_t *fb, uint32_t *fbc, hipStream_t st)
+{
+	struct xfg_kargs a;
+	pthread_mutex_lock(&ctx->lock);
+	ctx->reduced = 0;
+	int err = fill_kargs(ctx, d, sub, dv, &a);
+	pthread_mutex_unlock(&ctx->lock);
+	if (err)
+		return err;
+	if (hwin) {   /* header windows: the general kernel, listing what leaves them */
+		a.pipe = 0;
+		a.hwin = 1;
+		a.fb = fb;
+		a.fb_cnt = fbc;
+		a.fb_cap = HOST_CH;
+	}
+	return launch_batch(ctx, d, &a, st, 1);
+}
+
+/* The packets of the chunk at `c` whose programs left their windows (count
+ * in *d->hs_hfbc[k], list in d->hs_fb[k]): their whole frames through the
+ * ordinary path, FB_BYTES / FB_PKTS at a time; verdicts scattered back. */
+static int host_fallback(xfg_ctx *ctx, struct xfg_dev *d, const struct hsrc *src, uint64_t c,
+			 int k, uint8_t *verdicts)
+{
+	int err = 0;
+	const uint32_t nf = *d->hs_hfbc[k];
+	if (!nf)
+		return 0;
+	if (nf > HOST_CH)
+		return -EIO;
+	if ((err = fb_staging(d)))
+		return err;
+	HIPCHK(hipMemcpyAsync(d->fb_idx, d->hs_fb[k], (size_t)nf * 4, hipMemcpyDeviceToHost,
+			      d->hs_st[k]));
+	HIPCHK(hipStreamSynchronize(d->hs_st[k]));
+	for (uint32_t j0 = 0; j0 < nf;) {
+		uint64_t pos = 0;
+		uint32_t m = 0;
+		while (j0 + m < nf && m < FB_PKTS) {
+			const uint64_t gi = c + d->fb_idx[j0 + m];
+			const uint32_t l = hsrc_len(src, gi);
+			if (l > FB_BYTES)
+				return -E2BIG;
+			if (pos + l > FB_BYTES)
+				break;
+			memcpy(d->fb_h + pos, hsrc_ptr(src, gi), l);
+			d->fb_ho[m] = pos;
+			d->fb_hl[m] = l;
+			pos = (pos + l + 15) & ~15ull;   /* 16-byte aligned starts */
+			m++;
 		}
-		d->hs_bytes = 0;
-		for (int k = 0; k < 2; k++) {
-			HIPCHK(hipHostMalloc((void **)&d->hs_hbuf[k], chunk_bytes, hipHostMallocDefault));
-			HIPCHK(hipMalloc((void **)&d->hs_dbuf[k], chunk_bytes));
-		}
-		d->hs_bytes = chunk_bytes;
+		HIPCHK(hipMemcpyAsync(d->fb_d, d->fb_h, pos, hipMemcpyHostToDevice, d->hs_st[k]));
+		HIPCHK(hipMemcpyAsync(d->fb_do, d->fb_ho, (size_t)m * 8, hipMemcpyHostToDevice,
+				      d->hs_st[k]));
+		HIPCHK(hipMemcpyAsync(d->fb_dl, d->fb_hl, (size_t)m * 4, hipMemcpyHostToDevice,
+				      d->hs_st[k]));
+		struct xfg_batch sub = { d->fb_d, d->fb_do, d->fb_dl, m, 0, 0 };
+		if ((err = host_launch(ctx, d, &sub, d->fb_dv, 0, NULL, NULL, d->hs_st[k])))
+			return err;
+		/* (the pinned frame buffer doubles as the verdicts' landing place) */
+		HIPCHK(hipMemcpyAsync(d->fb_h, d->fb_dv, m, hipMemcpyDeviceToHost, d->hs_st[k]));
+		HIPCHK(hipStreamSynchronize(d->hs_st[k]));
+		for (uint32_t q = 0; q < m; q++)
+			verdicts[c + d->fb_idx[j0 + q]] = d->fb_h[q];
+		j0 += m;
+	}
+	*d->hs_hfbc[k] = 0;
+	return 0;
+fail:
+	return err;
+}
+
+static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, uint8_t *verdicts)
+{
+	int err = 0;
+	struct xfg_dev *d = &ctx->dev[dev];
+	/* whole slots: a fixed stride within the window (16-byte aligned, or
+	 * the kernel's 16-byte loads would straddle slots) */
+	const int whole = !src->descs && !src->offsets && src->stride && src->stride <= HOST_WIN &&
+			  !(src->stride & 15);
+	const uint32_t stride = whole ? src->stride : HOST_WIN;
+	uint64_t pend[2] = { UINT64_MAX, UINT64_MAX };   /* each slot's last chunk */
+
+	pthread_mutex_lock(&d->host_lock);
+	HIPCHK(hipSetDevice(d->ordinal));
+	if ((err = host_staging(d)))
+		goto fail;
+	for (uint64_t c = 0, k = 0; c < n; c += HOST_CH, k ^= 1) {
+		const uint64_t m = n - c < HOST_CH ? n - c : HOST_CH;
+		HIPCHK(hipEventSynchronize(d->hs_done[k]));   /* slot k free again */
+		if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
+			goto fail;
+		struct gather_job job = { src, c, m, d->hs_hbuf[k], d->hs_hl[k], stride, whole };
+		hpool_run(d->pool, gather_slice, &job);
+		HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], d->hs_hbuf[k], m * stride, hipMemcpyHostToDevice,
+				      d->hs_st[k]));
+		HIPCHK(hipMemcpyAsync(d->hs_dl[k], d->hs_hl[k], m * 4, hipMemcpyHostToDevice, d->hs_st[k]));
+		HIPCHK(hipMemsetAsync(d->hs_fbc[k], 0, 4, d->hs_st[k]));
+		struct xfg_batch sub = { d->hs_dbuf[k], NULL, d->hs_dl[k], m, stride, 0 };
+		if ((err = host_launch(ctx, d, &sub, d->hs_dv[k], !whole, d->hs_fb[k], d->hs_fbc[k],
+				       d->hs_st[k])))
+			goto fail;
+		HIPCHK(hipMemcpyAsync(verdicts + c, d->hs_dv[k], m, hipMemcpyDeviceToHost, d->hs_st[k]));
+		HIPCHK(hipMemcpyAsync(d->hs_hfbc[k], d->hs_fbc[k], 4, hipMemcpyDeviceToHost, d->hs_st[k]));
+		HIPCHK(hipEventRecord(d->hs_done[k], d->hs_st[k]));
+		pend[k] = whole ? UINT64_MAX : c;
+	}
+	for (int k = 0; k < 2; k++) {
+		HIPCHK(hipStreamSynchronize(d->hs_st[k]));
+		if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
+			goto fail;
 	}
 fail:
+	for (int k = 0; k < 2; k++)   /* (after an error: nothing may still use them) */
+		if (d->hs_st[k])
+			hipStreamSynchronize(d->hs_st[k]);
+	pthread_mutex_unlock(&d->host_lock);
 	return err;
 }
 
 int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t *verdicts)
 {
-	int err = 0;
-	if (!ctx || !b || (!verdicts && b->count))
+	if (!ctx || !b || (!verdicts && b->count) || (b->count && (!b->data || !b->lens)))
 		return -EINVAL;
 	if (!ctx->ndev)
 		return -ENODEV;
 	if (dev < 0 || dev >= ctx->ndev)
 		return -EINVAL;
+	if (!b->offsets && !b->stride && b->count)
+		return -EINVAL;
 	if (!b->count)
 		return 0;
-	struct xfg_dev *d = &ctx->dev[dev];
-	uint64_t maxlen = 0;
-	for (uint64_t i = 0; i < b->count; i++) {
-		uint64_t l = b->lens_u16 ? ((const uint16_t *)b->lens)[i] : ((const uint32_t *)b->lens)[i];
-		if (l > maxlen)
-			maxlen = l;
-	}
-	uint32_t stride = (uint32_t)((maxlen + 15) & ~15ull);
-	if (stride < 64)
-		stride = 64;
-	/* a fixed-stride batch whose stride fits is staged as it lies */
-	int contiguous = !b->offsets && b->stride >= stride && !(b->stride & 15);
-	if (contiguous)
-		stride = b->stride;
-	size_t chunk_bytes = (size_t)HOST_CH * stride;
+	const struct hsrc src = { b->data, b->offsets, b->stride, b->lens, b->lens_u16, NULL, 0, 0 };
+	return host_run(ctx, dev, &src, b->count, verdicts);
+}
 
-	pthread_mutex_lock(&ctx->host_lock);   /* the staging buffers are shared */
-	HIPCHK(hipSetDevice(d->ordinal));
-	if ((err = host_staging(d, chunk_bytes)))
-		goto fail;
-	for (uint64_t c = 0, k = 0; c < b->count; c += HOST_CH, k ^= 1) {
-		uint64_t m = b->count - c < HOST_CH ? b->count - c : HOST_CH;
-		HIPCHK(hipEventSynchronize(d->hs_done[k]));   /* staging buffer k free again */
-		repack(b, d->hs_hbuf[k], d->hs_hl[k], c, m, stride, contiguous);
-		HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], d->hs_hbuf[k], m * stride, hipMemcpyHostToDevice,
-				      d->hs_st[k]));
-		HIPCHK(hipMemcpyAsync(d->hs_dl[k], d->hs_hl[k], m * 4, hipMemcpyHostToDevice, d->hs_st[k]));
-		struct xfg_batch sub = { d->hs_dbuf[k], NULL, d->hs_dl[k], m, stride, 0 };
-		struct xfg_kargs a;
-		pthread_mutex_lock(&ctx->lock);
-		ctx->reduced = 0;
-		err = fill_kargs(ctx, d, &sub, d->hs_dv[k], &a);
-		pthread_mutex_unlock(&ctx->lock);
-		if (err)
-			goto fail;
-		/* copies on hs_st[k]; the kernels on the device stream (launch_batch
-		 * orders it after hs_st[k]'s uploads and hs_st[k] after the kernels) */
-		if ((err = launch_batch(ctx, d, &a, d->hs_st[k], 1)))
-			goto fail;
-		HIPCHK(hipMemcpyAsync(verdicts + c, d->hs_dv[k], m, hipMemcpyDeviceToHost, d->hs_st[k]));
-		HIPCHK(hipEventRecord(d->hs_done[k], d->hs_st[k]));
+int xfg_classify_xsk_host(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *b,
+			  uint64_t umem_bytes, uint8_t *verdicts)
+{
+	if (!ctx || !b || (!verdicts && b->count) || (b->count && (!b->umem || !b->descs)))
+		return -EINVAL;
+	if (!ctx->ndev)
+		return -ENODEV;
+	if (dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	if (b->mask != 0xffffffffu && (b->mask & (b->mask + 1)))
+		return -EINVAL;   /* a ring mask is 2^k - 1 */
+	if (b->count > (uint64_t)b->mask + 1)
+		return -EINVAL;
+	if (!b->count)
+		return 0;
+	const struct hsrc src = { b->umem, NULL, 0, NULL, 0, b->descs, b->first, b->mask };
+	/* every frame inside the UMEM (the kernel ring would have refused it) */
+	for (uint64_t i = 0; i < b->count; i++) {
+		const uint64_t a = ((const uint64_t *)b->descs)[2ull * ((b->first + (uint32_t)i) & b->mask)];
+		const uint64_t off = (a & ((1ull << 48) - 1)) + (a >> 48);
+		if (off + hsrc_len(&src, i) > umem_bytes)
+			return -EINVAL;
 	}
-	HIPCHK(hipStreamSynchronize(d->hs_st[0]));
-	HIPCHK(hipStreamSynchronize(d->hs_st[1]));
-fail:
-	for (int k = 0; k < 2; k++)   /* (after an error: nothing may still use them) */
-		if (d->hs_st[k])
-			hipStreamSynchronize(d->hs_st[k]);
-	pthread_mutex_unlock(&ctx->host_lock);
-	return err;
+	return host_run(ctx, dev, &src, b->count, verdicts);
 }
 
 /* ------------------------------------------------------------------ stats */

@@ -70,12 +70,19 @@ struct Pkt {
 	const uint32_t *row;    // LDS row: bytes [0, min(len, W)) valid
 	const uint8_t *g;       // packet start in HBM
 	uint32_t len;
+	// header-window batch (kargs.hwin): the slot holds only the window, so
+	// a read past it is not made -- it flags the packet here (returns 0)
+	uint32_t *oob = nullptr;
 
 	// Byte o (caller has checked o < len, as the reference does).
 	__device__ __forceinline__ uint32_t u8(uint32_t o) const
 	{
 		if (o < (uint32_t)W)
 			return reinterpret_cast<const uint8_t *>(row)[o];
+		if (oob) {
+			*oob = 1;
+			return 0;
+		}
 		return gbyte(g, o);
 	}
 	// Little-endian 32-bit load of bytes o..o+3 (o+3 < len).
@@ -84,6 +91,10 @@ struct Pkt {
 		if (o + 4 <= (uint32_t)W) {
 			uint32_t lo = row[o >> 2], hi = row[(o >> 2) + 1];
 			return __builtin_amdgcn_alignbyte(hi, lo, o & 3);
+		}
+		if (oob) {
+			*oob = 1;
+			return 0;
 		}
 		return gbyte(g, o) | (gbyte(g, o + 1) << 8) | (gbyte(g, o + 2) << 16) |
 		       (gbyte(g, o + 3) << 24);
@@ -94,6 +105,10 @@ struct Pkt {
 		if (o + 2 <= (uint32_t)W) {
 			uint32_t lo = row[o >> 2], hi = row[(o >> 2) + 1];
 			return __builtin_amdgcn_alignbyte(hi, lo, o & 3) & 0xffffu;
+		}
+		if (oob) {
+			*oob = 1;
+			return 0;
 		}
 		return gbyte(g, o) | (gbyte(g, o + 1) << 8);
 	}
@@ -1090,11 +1105,17 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 			const int pk = c / CPP, sub = c % CPP;
 			const uint64_t gi = base + pk;
 			pre[it] = u32x4{ 0, 0, 0, 0 };
-			if (gi < a.n && (uint32_t)sub * 16 < load_len(a, gi))
+			if (gi < a.n && (uint32_t)sub * 16 < load_len(a, gi) &&
+			    (a.offsets || a.descs || (uint32_t)sub * 16 < a.stride))
 				pre[it] = __builtin_nontemporal_load(
 					reinterpret_cast<const u32x4 *>(pkt_ptr(a, gi) + sub * 16));
 		}
 		plen = base + tid < a.n ? load_len(a, base + tid) : 0;
+		// a fixed-stride slot bounds its frame (a longer length would read
+		// the next slot or past the batch); header windows keep the true
+		// length
+		if (!a.offsets && !a.descs && !a.hwin)
+			plen = min(plen, a.stride);
 	};
 	if (tile < ntiles)
 		issue(tile);
@@ -1117,10 +1138,19 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 		const uint64_t gi = base + tid;
 		uint32_t act = A_NONE, tag = CT_NONE;
 		if (gi < a.n) {
-			Pkt<W> p{ &win[tid * ROWDW], pkt_ptr(a, gi), len };
+			uint32_t oob = 0;
+			Pkt<W> p{ &win[tid * ROWDW], pkt_ptr(a, gi), len, a.hwin ? &oob : nullptr };
 			const Parsed r = parse<FEAT, W>(p);
 			act = lookups<FEAT, false>(a, LazyKeys<Pkt<W>>{ p }, r, s_ports, tag);
-			a.verdicts[gi] = (uint8_t)act;
+			if (oob) {   // past the header window: the host's whole-frame pass
+				act = A_NONE;
+				tag = CT_NONE;
+				const uint32_t k = atomicAdd(a.fb_cnt, 1u);
+				if (k < a.fb_cap)
+					a.fb[k] = (uint32_t)gi;
+			} else {
+				a.verdicts[gi] = (uint8_t)act;
+			}
 		}
 		cn.bump(a, tag, lane);
 		st.add(act, len);

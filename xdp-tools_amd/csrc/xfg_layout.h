@@ -136,6 +136,15 @@ struct xfg_kargs {
 	uint32_t *defer;
 	uint32_t defer_cap;
 	uint32_t diag;                /* diagnostics build only (XFG_DIAG_MASK); 0 */
+	/* Header-window batches (xfg_classify_host): each slot holds only the
+	 * first `stride` bytes of its frame, lens are the frames' true lengths.
+	 * A packet whose program reads past the window is not classified here:
+	 * its index goes to fb (fb_cnt entries, at most fb_cap) and it is
+	 * counted nowhere; the host classifies it again from the whole frame. */
+	uint32_t hwin;                /* 1 = header-window batch; 0 = whole frames */
+	uint32_t fb_cap;
+	uint32_t *fb;
+	uint32_t *fb_cnt;
 };
 
 

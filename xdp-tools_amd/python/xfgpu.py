@@ -49,7 +49,7 @@ EXPORTS = [
     "xfg_sync", "xfg_dev_alloc", "xfg_dev_free", "xfg_memcpy_h2d", "xfg_memcpy_d2h",
     "xfg_host_alloc_pinned", "xfg_host_free_pinned", "xfg_classify_timed", "xfg_stream_read_timed",
     "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce", "xfg_map_update_batch_percpu",
-    "xfg_classify_descs", "xfg_compact",
+    "xfg_classify_descs", "xfg_compact", "xfg_classify_xsk_host",
 ]
 # include/xdpfilter_io.h
 IO_EXPORTS = [
@@ -127,6 +127,7 @@ def _load():
         "xfg_classify": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, vp]),
         "xfg_classify_host": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp]),
         "xfg_classify_descs": (C.c_int, [vp, C.c_int, C.POINTER(DescBatch), vp, vp]),
+        "xfg_classify_xsk_host": (C.c_int, [vp, C.c_int, C.POINTER(DescBatch), C.c_uint64, vp]),
         "xfg_compact": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
         "xfg_classify_timed": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, C.c_int,
                                          C.POINTER(C.c_double)]),
@@ -399,6 +400,18 @@ class Filter:
         b = DescBatch(umem_ptr, descs_ptr, first, mask, count)
         _check(lib.xfg_classify_descs(self.ctx, dev, C.byref(b), verdicts_ptr, stream),
                "classify_descs")
+
+    def classify_xsk_host(self, umem: np.ndarray, descs: np.ndarray, count, first=0,
+                          mask=0xffffffff, dev=0):
+        """AF_XDP RX ring + UMEM in host memory (xfg_classify_xsk_host);
+        descs: uint64 [entries, 2] xdp_desc records.  Returns verdicts."""
+        verdicts = np.zeros(count, np.uint8)
+        umem = np.ascontiguousarray(umem)
+        descs = np.ascontiguousarray(descs, np.uint64)
+        b = DescBatch(umem.ctypes.data, descs.ctypes.data, first, mask, count)
+        _check(lib.xfg_classify_xsk_host(self.ctx, dev, C.byref(b), umem.nbytes,
+                                         verdicts.ctypes.data), "classify_xsk_host")
+        return verdicts
 
     def compact(self, verdicts_ptr, n, action, idx_ptr, count_ptr, dev=0, stream=None):
         _check(lib.xfg_compact(self.ctx, dev, verdicts_ptr, n, action, idx_ptr, count_ptr, stream),
