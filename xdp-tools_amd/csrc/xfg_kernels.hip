@@ -866,7 +866,8 @@ __device__ __forceinline__ void log_append(uint32_t *region, uint32_t &cnt, uint
 // counting-sorted by partition in LDS and written out as per-partition runs
 // (consecutive lanes, consecutive addresses).  s: LDS scratch of
 // 4 * XFG_LOG_PARTS + LOG_CHUNK words.  Whole workgroup, after a barrier.
-constexpr uint32_t LOG_CHUNK = 4096;
+constexpr uint32_t LOG_CHUNK = 8192;
+constexpr uint32_t LOG_SCRATCH = 4 * XFG_LOG_PARTS + LOG_CHUNK;   // words
 
 template <int NW>
 __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t *s_n,
@@ -900,64 +901,75 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 		s_h[p] = 0;
 	}
 	__syncthreads();
+	// the NW regions as one sequence (entry e of region w at pre[w] + e),
+	// cut into chunks of LOG_CHUNK: runs of about LOG_CHUNK / 256 entries
+	uint32_t pre[NW + 1];
+	pre[0] = 0;
+#pragma unroll
+	for (int w = 0; w < NW; w++)
+		pre[w + 1] = pre[w] + s_n[w];
+	const uint32_t total = pre[NW];
 	const int lane = tid & 63;
-	for (int w = 0; w < NW; w++) {
-		const uint32_t *reg = a.tlog + r0 + (uint64_t)w * a.defer_cap;
-		const uint32_t nw = s_n[w];
-		for (uint32_t c0 = 0; c0 < nw; c0 += LOG_CHUNK) {
-			const uint32_t cn = min(LOG_CHUNK, nw - c0);
-			// rank each entry within its partition
-			uint32_t g[K], rk[K];
+	for (uint32_t c0 = 0; c0 < total; c0 += LOG_CHUNK) {
+		const uint32_t cn = min(LOG_CHUNK, total - c0);
+		// rank each entry within its partition
+		uint32_t g[K], rk[K];
 #pragma unroll
-			for (int j = 0; j < K; j++) {
-				const uint32_t e = tid + j * NTH;
-				g[j] = e < cn ? reg[c0 + e] : CT_NONE;
-				rk[j] = g[j] != CT_NONE ? atomicAdd(&s_h[log_part(g[j])], 1u) : 0u;
+		for (int j = 0; j < K; j++) {
+			const uint32_t e = c0 + tid + j * NTH;
+			g[j] = CT_NONE;
+			if (e < total) {
+				int w = 0;
+#pragma unroll
+				for (int q = 1; q < NW; q++)
+					w += e >= pre[q];
+				g[j] = a.tlog[r0 + (uint64_t)w * a.defer_cap + (e - pre[w])];
 			}
-			__syncthreads();
-			// run starts: exclusive scan of the counts (one wave)
-			if (tid < 64) {
-				uint32_t v[XFG_LOG_PARTS / 64], sum = 0;
-#pragma unroll
-				for (int q = 0; q < (int)(XFG_LOG_PARTS / 64); q++) {
-					v[q] = s_h[lane * (XFG_LOG_PARTS / 64) + q];
-					sum += v[q];
-				}
-				uint32_t inc = sum;
-#pragma unroll
-				for (int o = 1; o < 64; o <<= 1) {
-					const uint32_t y = __shfl_up(inc, o);
-					if (lane >= o)
-						inc += y;
-				}
-				uint32_t run = inc - sum;
-#pragma unroll
-				for (int q = 0; q < (int)(XFG_LOG_PARTS / 64); q++) {
-					s_off[lane * (XFG_LOG_PARTS / 64) + q] = run;
-					run += v[q];
-				}
-			}
-			__syncthreads();
-#pragma unroll
-			for (int j = 0; j < K; j++)
-				if (g[j] != CT_NONE)
-					s_srt[s_off[log_part(g[j])] + rk[j]] = g[j];
-			__syncthreads();
-			for (uint32_t t = tid; t < cn; t += nthr) {
-				const uint32_t x = s_srt[t], p = log_part(x);
-				const uint32_t pos = s_b[p] + s_cur[p] + (t - s_off[p]);
-				if (pos < a.pcap)
-					a.pbuf[(uint64_t)p * a.pcap + pos] = x;
-				else
-					atomicAdd(global_counter(a, x), 1ull);
-			}
-			__syncthreads();
-			for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
-				s_cur[p] += s_h[p];
-				s_h[p] = 0;
-			}
-			__syncthreads();
+			rk[j] = g[j] != CT_NONE ? atomicAdd(&s_h[log_part(g[j])], 1u) : 0u;
 		}
+		__syncthreads();
+		// run starts: exclusive scan of the counts (one wave)
+		if (tid < 64) {
+			uint32_t v[XFG_LOG_PARTS / 64], sum = 0;
+#pragma unroll
+			for (int q = 0; q < (int)(XFG_LOG_PARTS / 64); q++) {
+				v[q] = s_h[lane * (XFG_LOG_PARTS / 64) + q];
+				sum += v[q];
+			}
+			uint32_t inc = sum;
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const uint32_t y = __shfl_up(inc, o);
+				if (lane >= o)
+					inc += y;
+			}
+			uint32_t run = inc - sum;
+#pragma unroll
+			for (int q = 0; q < (int)(XFG_LOG_PARTS / 64); q++) {
+				s_off[lane * (XFG_LOG_PARTS / 64) + q] = run;
+				run += v[q];
+			}
+		}
+		__syncthreads();
+#pragma unroll
+		for (int j = 0; j < K; j++)
+			if (g[j] != CT_NONE)
+				s_srt[s_off[log_part(g[j])] + rk[j]] = g[j];
+		__syncthreads();
+		for (uint32_t t = tid; t < cn; t += nthr) {
+			const uint32_t x = s_srt[t], p = log_part(x);
+			const uint32_t pos = s_b[p] + s_cur[p] + (t - s_off[p]);
+			if (pos < a.pcap)
+				a.pbuf[(uint64_t)p * a.pcap + pos] = x;
+			else
+				atomicAdd(global_counter(a, x), 1ull);
+		}
+		__syncthreads();
+		for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
+			s_cur[p] += s_h[p];
+			s_h[p] = 0;
+		}
+		__syncthreads();
 	}
 }
 

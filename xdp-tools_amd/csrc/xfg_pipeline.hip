@@ -389,7 +389,8 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 	constexpr int ROWDW = W / 4 + 1;        // odd dword stride per LDS row
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
-	__shared__ uint32_t win[NW * 64 * ROWDW];
+	// the wave rows; after the loop, the hit-log partition scratch
+	__shared__ uint32_t win[NW * 64 * ROWDW > LOG_SCRATCH ? NW * 64 * ROWDW : LOG_SCRATCH];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
 	__shared__ unsigned long long s_stats[6];
@@ -682,7 +683,6 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
 	cn.flush(a, tid, NT);
-	static_assert(NW * 64 * ROWDW >= 4 * XFG_LOG_PARTS + LOG_CHUNK, "partition scratch");
 	if (a.tlog)   // (win is free now: the partition scratch)
 		log_partition<NW>(a, s_tn, nullptr, win, tid);
 }
@@ -801,7 +801,8 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
-	__shared__ uint32_t win[NW * 64 * ROWDW];
+	// the wave rows; after the loop, the hit-log partition scratch
+	__shared__ uint32_t win[NW * 64 * ROWDW > LOG_SCRATCH ? NW * 64 * ROWDW : LOG_SCRATCH];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
 	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB : 1];   // per port-table slot
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
@@ -1172,7 +1173,6 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 			for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
 				if (s_pcnt[i])
 					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
-	static_assert(NW * 64 * ROWDW >= 4 * XFG_LOG_PARTS + LOG_CHUNK, "partition scratch");
 	if (a.tlog && !(dg & 16))   // (win is free now: the partition scratch)
 		log_partition<NW>(a, s_tn, s_lh, win, tid);
 }
