@@ -9,11 +9,12 @@ JOBS ?= 8
 
 all: product synth oracle diag
 
-diag:
-	$(MAKE) -C xdp-tools_amd diag
+diag: product
 
+# (one sub-make for the product and the diagnostics library: their two
+# kernel objects compile in parallel, the shared host objects once)
 product:
-	$(MAKE) -C xdp-tools_amd -j$(JOBS)
+	$(MAKE) -C xdp-tools_amd -j$(JOBS) all diag
 
 synth: tools/libxfsynth.so
 
