@@ -7,7 +7,9 @@
       shard of the 8-GPU configuration (weak scaling: per-GPU work fixed)
   c5  xdpfilt_dny_all, 1514 B frames, 15M IPv4 + 1M IPv6 dst rules + 1024
       dst-port rules: device-resident, and end to end from host memory
-      (whole frames H2D, verdicts D2H, xfg_classify_host)
+      (header windows H2D, verdicts D2H, xfg_classify_host)
+  c3sd  C3 with every rule src|dst (`-m src,dst`): both IPv4 lookups live,
+      so a packet probes two keys (the case C3's all-dst census skips)
 
 Roofline bytes per packet are min(len, 128) + 1.
 Usage: python3 tools/bench_configs.py [c2] [c4] [c5] [--log2-packets N]
@@ -29,10 +31,11 @@ def run(name, args):
     import numpy as np
     import xftools as X
     import xfgpu as G
-    kind = {"c2": 2, "c4": 4, "c5": 5}[name]
-    n = 1 << (args.log2_packets or {"c2": 24, "c4": 21, "c5": 20}[name])
-    stride = 64 if kind == 2 else 1536
-    n4 = {2: 1000, 4: 1_000_000, 5: 15_000_000}[kind]
+    kind = {"c2": 2, "c4": 4, "c5": 5, "c3sd": 3}[name]
+    n = 1 << (args.log2_packets or {"c2": 24, "c4": 21, "c5": 20, "c3sd": 24}[name])
+    stride = 64 if kind in (2, 3) else 1536
+    n4 = {2: 1000, 3: 1_000_000, 4: 1_000_000, 5: 15_000_000}[kind]
+    flag = 3 if name == "c3sd" else 2
     n6 = 1_000_000 if kind == 5 else 0
     nports = 1024 if kind == 5 else 16
     t0 = time.time()
@@ -44,7 +47,7 @@ def run(name, args):
     print(f"[{name}] frames {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     feats = G.FEAT_IPV4 | G.FEAT_IPV6 | G.FEAT_DENY if kind == 2 else G.FEAT_ALL | G.FEAT_DENY
     f = G.Filter(feats, devices=[0], ipv4_capacity=n4, ipv6_capacity=max(n6, 1024))
-    f.update_batch(G.MAP_IPV4, v4, np.full(len(v4), 2, np.uint64))
+    f.update_batch(G.MAP_IPV4, v4, np.full(len(v4), flag, np.uint64))
     if n6:
         f.update_batch(G.MAP_IPV6, v6, np.full(len(v6), 2, np.uint64))
     if kind != 2:
@@ -87,7 +90,7 @@ def run(name, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("configs", nargs="*", default=["c2", "c4", "c5"])
+    ap.add_argument("configs", nargs="*", default=["c2", "c4", "c5", "c3sd"])
     ap.add_argument("--log2-packets", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()

@@ -959,6 +959,8 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 		for (uint32_t t = tid; t < cn; t += nthr) {
 			const uint32_t x = s_srt[t], p = log_part(x);
 			const uint32_t pos = s_b[p] + s_cur[p] + (t - s_off[p]);
+			if (a.diag & 256)   // diagnostics build only: no write-out
+				continue;
 			if (pos < a.pcap)
 				a.pbuf[(uint64_t)p * a.pcap + pos] = x;
 			else
@@ -1182,7 +1184,7 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 // in an LDS histogram, then adds each non-zero count to its counter with a
 // plain read-modify-write (the workgroup owns the partition's counters),
 // and resets the partition's fill for the next launch.
-constexpr int LC_THREADS = 512;
+constexpr int LC_THREADS = 1024;
 
 __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kargs a, uint32_t hist_n)
 {
