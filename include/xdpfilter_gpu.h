@@ -202,6 +202,17 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
 		      uint8_t *verdicts);
 
 /*
+ * Register a long-lived host buffer (a capture ring, an AF_XDP UMEM) for
+ * direct DMA: a host batch whose fixed-stride slots (stride <= 128) lie
+ * inside a registered buffer is copied to the device where it lies, with
+ * no staging copy.  Pins the pages (hipHostRegister) until
+ * xfg_host_unregister() or xfg_close().  At most 16 buffers per context;
+ * -EEXIST if it overlaps a registered one.
+ */
+int xfg_host_register(xfg_ctx *ctx, void *p, size_t bytes);
+int xfg_host_unregister(xfg_ctx *ctx, void *p);
+
+/*
  * AF_XDP RX in host memory: the consumer side of an XDP socket's RX ring
  * (xsk_ring_cons__peek() / xsk_ring_cons__rx_desc() / xsk_ring_cons__release(),
  * headers/xdp/xsk.h:80-86,143-165).  Packet i is ring record

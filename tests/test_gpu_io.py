@@ -479,3 +479,33 @@ def test_cli_run_capture_with_one_huge_frame(G, cli, tmp_path):
     assert len(got[1234][0]) == len(huge)
     np.testing.assert_array_equal([g[2] for g in got], ov)
     cli("unload", "veth0")
+
+
+def test_classify_host_registered_buffer(G):
+    """xfg_host_register: a registered 64-byte-stride batch is copied to the
+    device where it lies (no staging copy); same verdicts, counters and
+    stats; overlapping registration and unknown unregister are refused."""
+    n = (1 << 19) + 5
+    v4 = X.rand_keys(3, 20000, 4)
+    ports = np.array([53, 80], np.uint16)
+    data, lens = X.gen_workload(3, 3, n, 64, v4=v4, ports=ports)
+    rules = X.RuleSet()
+    rules.v4_keys, rules.v4_vals = v4, np.full(len(v4), 2, np.uint64)
+    for p in ports:
+        rules.ports[X.port_key(int(p))] = 2 | 4 | 8
+    feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    ov, orules, ost = X.run_oracle(feats, data, lens, rules, stride=64, nthreads=8)
+    f = G.Filter(feats, ndev=1, ipv4_capacity=len(v4))
+    f.load_rules(rules)
+    f.host_register(data)
+    with pytest.raises(OSError):
+        f.host_register(data[64:])            # overlaps
+    v = f.classify_host(data, lens.astype(np.uint16), stride=64)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(f.stats(), ost)
+    r = rules.prepared()
+    np.testing.assert_array_equal(f.values_of(G.MAP_IPV4, r.v4_keys), orules.v4_vals)
+    f.host_unregister(data)
+    with pytest.raises(OSError):
+        f.host_unregister(data)
+    f.close()

@@ -39,6 +39,7 @@ int xfg_launch_compact(const uint8_t *verdicts, uint64_t n, uint32_t action, uin
 uint64_t xfg_compact_tiles(uint64_t n);
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
+#define XFG_HOST_REG_MAX 16 /* registered host buffers per context */
 
 struct dev_map {           /* device arrays of one hash map */
 	uint8_t *buckets;      /* (nbuckets + 1) * 64 B: keys, per-device flags, meta */
@@ -119,6 +120,10 @@ struct xfg_ctx {
 	ncclComm_t comm;
 	int comm_ready;
 	int reduced;
+	/* host buffers registered for direct DMA (xfg_host_register) */
+	pthread_mutex_t reg_lock;
+	struct { const uint8_t *p; size_t bytes; } reg[XFG_HOST_REG_MAX];
+	int nreg;
 };
 
 /* ------------------------------------------------------------------ misc */
@@ -421,6 +426,7 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 	if (!ctx)
 		return -ENOMEM;
 	pthread_mutex_init(&ctx->lock, NULL);
+	pthread_mutex_init(&ctx->reg_lock, NULL);
 	err = xfg_select_program(opts->features, &ctx->prog_name, &ctx->prog_features);
 	if (err)
 		goto fail;
@@ -496,6 +502,9 @@ void xfg_close(xfg_ctx *ctx)
 		ncclCommDestroy(ctx->comm);
 	for (int i = 0; i < ctx->ndev && ctx->dev; i++)
 		dev_free(&ctx->dev[i]);
+	for (int i = 0; i < ctx->nreg; i++)
+		hipHostUnregister((void *)ctx->reg[i].p);
+	pthread_mutex_destroy(&ctx->reg_lock);
 	free(ctx->dev);
 	for (int i = 0; i < NMAPS_HASH; i++) {
 		xfg_table_free(&ctx->t[i]);
@@ -1470,7 +1479,9 @@ struct gather_job {
 	uint8_t *dst;
 	uint32_t *dl;
 	uint32_t stride;           /* staging stride: HOST_WIN, or the batch's */
-	int whole;                 /* whole slots (stride <= HOST_WIN, no offsets) */
+	int whole;                 /* 1 whole slots copied (stride <= HOST_WIN, no
+				    * offsets), 2 whole slots left where they lie
+				    * (registered memory: lengths only), 0 windows */
 };
 
 static void gather_slice(void *arg, int t, int nt)
@@ -1480,7 +1491,7 @@ static void gather_slice(void *arg, int t, int nt)
 	const uint64_t s0 = t * per, s1 = s0 + per < j->m ? s0 + per : j->m;
 	if (s0 >= s1)
 		return;
-	if (j->whole)
+	if (j->whole == 1)
 		memcpy(j->dst + s0 * j->stride, j->src->data + (j->first + s0) * j->stride,
 		       (s1 - s0) * j->stride);
 	for (uint64_t i = s0; i < s1; i++) {
@@ -1640,6 +1651,65 @@ fail:
 	return err;
 }
 
+/* ---- registered host buffers: DMA straight from the caller's memory */
+int xfg_host_register(xfg_ctx *ctx, void *p, size_t bytes)
+{
+	int err = 0;
+	if (!ctx || !p || !bytes)
+		return -EINVAL;
+	pthread_mutex_lock(&ctx->reg_lock);
+	for (int i = 0; i < ctx->nreg; i++) {
+		const uint8_t *a = ctx->reg[i].p, *b = (const uint8_t *)p;
+		if (b < a + ctx->reg[i].bytes && a < b + bytes) {
+			err = -EEXIST;   /* overlaps a registered buffer */
+			goto out;
+		}
+	}
+	if (ctx->nreg == XFG_HOST_REG_MAX) {
+		err = -ENOSPC;
+		goto out;
+	}
+	if ((err = hip_err(hipHostRegister(p, bytes, hipHostRegisterPortable))))
+		goto out;
+	ctx->reg[ctx->nreg].p = p;
+	ctx->reg[ctx->nreg].bytes = bytes;
+	ctx->nreg++;
+out:
+	pthread_mutex_unlock(&ctx->reg_lock);
+	return err;
+}
+
+int xfg_host_unregister(xfg_ctx *ctx, void *p)
+{
+	int err = -ENOENT;
+	if (!ctx || !p)
+		return -EINVAL;
+	/* (no host-path call may be using it: the caller's contract, as for
+	 * freeing any buffer it passed) */
+	pthread_mutex_lock(&ctx->reg_lock);
+	for (int i = 0; i < ctx->nreg; i++) {
+		if (ctx->reg[i].p != p)
+			continue;
+		err = hip_err(hipHostUnregister(p));
+		ctx->reg[i] = ctx->reg[--ctx->nreg];
+		break;
+	}
+	pthread_mutex_unlock(&ctx->reg_lock);
+	return err;
+}
+
+/* Whether [p, p + bytes) lies inside one registered buffer. */
+static int host_registered(xfg_ctx *ctx, const void *p, uint64_t bytes)
+{
+	int r = 0;
+	pthread_mutex_lock(&ctx->reg_lock);
+	for (int i = 0; i < ctx->nreg && !r; i++)
+		r = (const uint8_t *)p >= ctx->reg[i].p &&
+		    (const uint8_t *)p + bytes <= ctx->reg[i].p + ctx->reg[i].bytes;
+	pthread_mutex_unlock(&ctx->reg_lock);
+	return r;
+}
+
 static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, uint8_t *verdicts)
 {
 	int err = 0;
@@ -1649,6 +1719,8 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 	const int whole = !src->descs && !src->offsets && src->stride && src->stride <= HOST_WIN &&
 			  !(src->stride & 15);
 	const uint32_t stride = whole ? src->stride : HOST_WIN;
+	/* whole slots in a registered buffer: copied by DMA where they lie */
+	const int direct = whole && host_registered(ctx, src->data, n * (uint64_t)stride);
 	uint64_t pend[2] = { UINT64_MAX, UINT64_MAX };   /* each slot's last chunk */
 
 	pthread_mutex_lock(&d->host_lock);
@@ -1660,10 +1732,12 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 		HIPCHK(hipEventSynchronize(d->hs_done[k]));   /* slot k free again */
 		if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
 			goto fail;
-		struct gather_job job = { src, c, m, d->hs_hbuf[k], d->hs_hl[k], stride, whole };
+		struct gather_job job = { src, c, m, d->hs_hbuf[k], d->hs_hl[k], stride, whole && !direct };
+		if (direct)   /* (the slots go by DMA: only the lengths are gathered) */
+			job.whole = 2;
 		hpool_run(d->pool, gather_slice, &job);
-		HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], d->hs_hbuf[k], m * stride, hipMemcpyHostToDevice,
-				      d->hs_st[k]));
+		HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], direct ? src->data + c * stride : d->hs_hbuf[k],
+				      m * stride, hipMemcpyHostToDevice, d->hs_st[k]));
 		HIPCHK(hipMemcpyAsync(d->hs_dl[k], d->hs_hl[k], m * 4, hipMemcpyHostToDevice, d->hs_st[k]));
 		HIPCHK(hipMemsetAsync(d->hs_fbc[k], 0, 4, d->hs_st[k]));
 		struct xfg_batch sub = { d->hs_dbuf[k], NULL, d->hs_dl[k], m, stride, 0 };

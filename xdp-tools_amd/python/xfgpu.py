@@ -49,7 +49,8 @@ EXPORTS = [
     "xfg_sync", "xfg_dev_alloc", "xfg_dev_free", "xfg_memcpy_h2d", "xfg_memcpy_d2h",
     "xfg_host_alloc_pinned", "xfg_host_free_pinned", "xfg_classify_timed", "xfg_stream_read_timed",
     "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce", "xfg_map_update_batch_percpu",
-    "xfg_classify_descs", "xfg_compact", "xfg_classify_xsk_host",
+    "xfg_classify_descs", "xfg_compact", "xfg_classify_xsk_host", "xfg_host_register",
+    "xfg_host_unregister",
 ]
 # include/xdpfilter_io.h
 IO_EXPORTS = [
@@ -128,6 +129,8 @@ def _load():
         "xfg_classify_host": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp]),
         "xfg_classify_descs": (C.c_int, [vp, C.c_int, C.POINTER(DescBatch), vp, vp]),
         "xfg_classify_xsk_host": (C.c_int, [vp, C.c_int, C.POINTER(DescBatch), C.c_uint64, vp]),
+        "xfg_host_register": (C.c_int, [vp, vp, C.c_size_t]),
+        "xfg_host_unregister": (C.c_int, [vp, vp]),
         "xfg_compact": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
         "xfg_classify_timed": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, C.c_int,
                                          C.POINTER(C.c_double)]),
@@ -400,6 +403,13 @@ class Filter:
         b = DescBatch(umem_ptr, descs_ptr, first, mask, count)
         _check(lib.xfg_classify_descs(self.ctx, dev, C.byref(b), verdicts_ptr, stream),
                "classify_descs")
+
+    def host_register(self, arr: np.ndarray):
+        """Pin a long-lived host array for direct DMA (xfg_host_register)."""
+        _check(lib.xfg_host_register(self.ctx, arr.ctypes.data, arr.nbytes), "host_register")
+
+    def host_unregister(self, arr: np.ndarray):
+        _check(lib.xfg_host_unregister(self.ctx, arr.ctypes.data), "host_unregister")
 
     def classify_xsk_host(self, umem: np.ndarray, descs: np.ndarray, count, first=0,
                           mask=0xffffffff, dev=0):
