@@ -16,7 +16,7 @@ import json
 import os
 import sys
 
-os.environ["XFG_LIB"] = "diag"
+os.environ.setdefault("XFG_LIB", "diag")   # or a library file (A/B runs)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))

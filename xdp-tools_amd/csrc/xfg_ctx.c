@@ -68,9 +68,10 @@ struct xfg_dev {
 	uint32_t port_tab_disp;
 	int port_tab_ok, port_tab_dirty;
 	/* resident classify workgroups per CU: [kernel: 0 general, 1 pipelined,
-	 * 2 pipelined IPv4-key mode][window 64, 128][dynamic LDS: none, direct
-	 * counters, port nibble map, both] */
-	int occ[3][2][4];
+	 * 2 pipelined IPv4-key mode, 3 split lookup pass, 4 split parse pass]
+	 * [window 64, 128][dynamic LDS: none, direct counters, port nibble map,
+	 * both] */
+	int occ[5][2][4];
 	/* host-resident classify (xfg_classify_host / xfg_classify_xsk_host),
 	 * under host_lock: a gather pool, two fixed-size staging slots of
 	 * HOST_CH packets x HOST_WIN bytes (header windows, or whole slots of
@@ -92,6 +93,8 @@ struct xfg_dev {
 	uint64_t defer_bytes;
 	uint32_t *tlog, *pbuf, *pfill;  /* hit log: wave regions, partition buffers, fills */
 	uint64_t tlog_bytes, pbuf_bytes;
+	uint32_t *rec;                  /* split classify: parse-pass records */
+	uint64_t rec_bytes;
 	unsigned long long *cstatus;    /* verdict compaction: tile status words */
 	uint64_t cstatus_cap;
 	uint32_t *cticket;
@@ -347,6 +350,7 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->defer);
 	hipFree(d->tlog);
 	hipFree(d->pbuf);
+	hipFree(d->rec);
 	hipFree(d->pfill);
 	hipFree(d->cticket);
 	if (d->ev_user)
@@ -402,7 +406,7 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	d->port_tab_dirty = 1;
 	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
-	for (int k = 0; k < 3; k++)
+	for (int k = 0; k < 5; k++)
 		for (int w = 0; w < 2; w++)
 			for (int c = 0; c < 4; c++)
 				d->occ[k][w][c] = xfg_classify_occupancy(
@@ -1143,6 +1147,12 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	const char *dm = getenv("XFG_DIAG_MASK");   /* pipelined IPv4-key kernel: drop a cost */
 	if (dm && *dm)
 		a->diag = (uint32_t)strtoul(dm, NULL, 0);
+	const char *kk = getenv("XFG_KERNEL");   /* "split": parse + lookup passes */
+	if (kk && !strcmp(kk, "split"))
+		a->split = a->pipe && a->km;
+	const char *bo = getenv("XFG_BLOOM");    /* "off": lookup pass without the prefilter */
+	if (bo && !strcmp(bo, "off") && !(a->t4.count && (a->t4.fmask & 3) == 3))
+		a->bloom_off = 1;
 	const char *em = getenv("XFG_EMPTY");   /* every table empty: stream + parse only */
 	if (em && !strcmp(em, "1")) {
 		a->t4.count = a->t6.count = a->te.count = 0;
@@ -1180,7 +1190,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 {
 	int err = 0;
 	struct xfg_kargs a = *a0;
-	const int kind = a.pipe ? (a.km ? 2 : 1) : 0, wi = a.window > 64;
+	const int kind = a.pipe ? (a.km ? (a.split ? 3 : 2) : 1) : 0, wi = a.window > 64;
 	const char *cm = NULL;
 #ifdef XFG_DIAG
 	cm = getenv("XFG_COUNT");   /* diagnostics build only: "atomic" */
@@ -1203,7 +1213,25 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	if (grid > need)
 		grid = need ? need : 1;
 
+	if (a.split) {
+		/* the parse pass: its own persistent grid */
+		uint64_t gp = (uint64_t)d->ncu * (d->occ[4][wi][0] > 0 ? d->occ[4][wi][0] : 1);
+		uint64_t tpw = (uint64_t)xfg_classify_threads(4, a.window);   /* packets per round */
+		uint64_t np = (a.n + tpw - 1) / tpw;
+		a.grid_parse = (uint32_t)(gp < np ? gp : (np ? np : 1));
+	}
+
 	pthread_mutex_lock(&d->lock);
+	if (a.split) {
+		/* parse-pass records: key a, ports, key b (both directions live) */
+		int both = a.t4.count && (a.t4.fmask & 3) == 3;
+		uint64_t per = (uint64_t)a.n * 4;
+		if ((err = scratch(d, (void **)&d->rec, &d->rec_bytes, per * (both ? 3 : 2))))
+			goto out;
+		a.rec_ka = d->rec;
+		a.rec_port = d->rec + a.n;
+		a.rec_kb = both ? d->rec + 2 * a.n : NULL;
+	}
 	if (a.pipe) {
 		/* one deferred list per wave, room for every packet of its tiles */
 		uint64_t nw = grid * (per_wg / 64), nt = (a.n + 63) / 64;

@@ -1178,6 +1178,9 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 }
 
 #include "xfg_pipeline.hip"
+#ifdef XFG_DIAG   // measured slower than xfg_pipe4_kernel: diagnostics only
+#include "xfg_split.hip"
+#endif
 
 // ---------------------------------------------------------------- hit-log count
 // One workgroup per log partition (see HitLog): sums the partition's buffer
@@ -1229,6 +1232,25 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 		bool done = false;
 		if constexpr ((FEAT & F_IPV4) != 0) {
 			// key mode 1 (only IPv4 keys live): the branch-free kernel
+			// (diagnostics build: or the split parse + lookup passes)
+#ifdef XFG_DIAG
+			if (a.km == 1 && a.split) {
+				done = true;
+				const dim3 gp(a.grid_parse), tp(64 * PARSE_WAVES);
+				if (a.window <= 64 && a.dense)
+					hipLaunchKernelGGL((xfg_parse4_kernel<FEAT, 64, true>), gp, tp, 0, s, a);
+				else if (a.window <= 64)
+					hipLaunchKernelGGL((xfg_parse4_kernel<FEAT, 64, false>), gp, tp, 0, s, a);
+				else if (a.dense)
+					hipLaunchKernelGGL((xfg_parse4_kernel<FEAT, 128, true>), gp, tp, 0, s, a);
+				else
+					hipLaunchKernelGGL((xfg_parse4_kernel<FEAT, 128, false>), gp, tp, 0, s, a);
+				if (a.window <= 64)
+					hipLaunchKernelGGL((xfg_look4_kernel<FEAT, 64>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
+				else
+					hipLaunchKernelGGL((xfg_look4_kernel<FEAT, 128>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
+			} else
+#endif
 			if (a.km == 1) {
 				done = true;
 				if (a.window <= 64 && a.dense)
@@ -1302,6 +1324,19 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 	hipError_t e = hipSuccess;
 	bool done = false;
 	if constexpr ((FEAT & F_IPV4) != 0) {
+#ifdef XFG_DIAG
+		if (kind == 3) {        // split: the lookup pass
+			done = true;
+			e = window <= 64
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_look4_kernel<FEAT, 64>, PIPE_THREADS(64), dyn)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_look4_kernel<FEAT, 128>, PIPE_THREADS(128), dyn);
+		} else if (kind == 4) { // split: the parse pass (no dynamic LDS)
+			done = true;
+			e = window <= 64
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_parse4_kernel<FEAT, 64, true>, 64 * PARSE_WAVES, 0)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_parse4_kernel<FEAT, 128, false>, 64 * PARSE_WAVES, 0);
+		} else
+#endif
 		if (kind == 2) {
 			done = true;
 			e = window <= 64
@@ -1342,6 +1377,8 @@ extern "C" int xfg_classify_occupancy(uint32_t prog_features, int kind, uint32_t
 // Threads per workgroup of a classify kernel (host grid sizing).
 extern "C" int xfg_classify_threads(int kind, uint32_t window)
 {
+	if (kind == 4)
+		return 256;   // the split parse pass (diagnostics build)
 	return kind >= 1 ? (window <= 64 ? PIPE_THREADS(64) : PIPE_THREADS(128)) : TILE;
 }
 

@@ -145,6 +145,16 @@ struct xfg_kargs {
 	uint32_t fb_cap;
 	uint32_t *fb;
 	uint32_t *fb_cnt;
+	/* Split IPv4-key classify (diagnostics build, xfg_split.hip): the parse
+	 * pass (grid_parse workgroups) writes per-packet records -- a state byte
+	 * in the verdict buffer, the first live key, the ports (dst | src << 16)
+	 * and, with both directions live, the second key -- that the lookup pass
+	 * reads.  bloom_off: the lookup pass goes to the bucket line without the
+	 * prefilter (one live key per packet only). */
+	uint32_t split;
+	uint32_t grid_parse;
+	uint32_t bloom_off;
+	uint32_t *rec_ka, *rec_kb, *rec_port;
 };
 
 

@@ -29,9 +29,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # XFG_LIB=diag selects the diagnostics build (measurement knobs; tools/ only),
 # XFG_LIB=asan the sanitizer build of the host C (the CPU suite under
 # tools/asan_suite.sh)
+# tools/ A/B runs may also name a library file outright (XFG_LIB=/path/x.so)
 _LIBS = {"diag": ("lib", "libxdpfilter_gpu_diag.so"), "asan": ("lib-asan", "libxdpfilter_gpu.so")}
-LIB_PATH = os.path.join(os.path.dirname(HERE),
-                        *_LIBS.get(os.environ.get("XFG_LIB", ""), ("lib", "libxdpfilter_gpu.so")))
+_SEL = os.environ.get("XFG_LIB", "")
+LIB_PATH = (_SEL if _SEL.endswith(".so") and os.path.isfile(_SEL) else
+            os.path.join(os.path.dirname(HERE), *_LIBS.get(_SEL, ("lib", "libxdpfilter_gpu.so"))))
 
 FEAT_TCP, FEAT_UDP, FEAT_IPV6, FEAT_IPV4, FEAT_ETHERNET = 1, 2, 4, 8, 16
 FEAT_ALL = 31
