@@ -910,10 +910,10 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 		pre[w + 1] = pre[w] + s_n[w];
 	const uint32_t total = pre[NW];
 	const int lane = tid & 63;
-	for (uint32_t c0 = 0; c0 < total; c0 += LOG_CHUNK) {
-		const uint32_t cn = min(LOG_CHUNK, total - c0);
-		// rank each entry within its partition
-		uint32_t g[K], rk[K];
+	// a chunk's entries; the next chunk's are in flight during the current
+	// chunk's write-out
+	uint32_t g[K], rk[K];
+	auto fetch = [&](uint32_t c0) {
 #pragma unroll
 		for (int j = 0; j < K; j++) {
 			const uint32_t e = c0 + tid + j * NTH;
@@ -925,8 +925,16 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 					w += e >= pre[q];
 				g[j] = a.tlog[r0 + (uint64_t)w * a.defer_cap + (e - pre[w])];
 			}
-			rk[j] = g[j] != CT_NONE ? atomicAdd(&s_h[log_part(g[j])], 1u) : 0u;
 		}
+	};
+	if (total)
+		fetch(0);
+	for (uint32_t c0 = 0; c0 < total; c0 += LOG_CHUNK) {
+		const uint32_t cn = min(LOG_CHUNK, total - c0);
+		// rank each entry within its partition
+#pragma unroll
+		for (int j = 0; j < K; j++)
+			rk[j] = g[j] != CT_NONE ? atomicAdd(&s_h[log_part(g[j])], 1u) : 0u;
 		__syncthreads();
 		// run starts: exclusive scan of the counts (one wave)
 		if (tid < 64) {
@@ -955,6 +963,8 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 		for (int j = 0; j < K; j++)
 			if (g[j] != CT_NONE)
 				s_srt[s_off[log_part(g[j])] + rk[j]] = g[j];
+		if (c0 + LOG_CHUNK < total)
+			fetch(c0 + LOG_CHUNK);
 		__syncthreads();
 		for (uint32_t t = tid; t < cn; t += nthr) {
 			const uint32_t x = s_srt[t], p = log_part(x);

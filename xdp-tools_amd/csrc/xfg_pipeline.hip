@@ -1131,6 +1131,10 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	if (k < iters)
 		iteration(k, preA, lenA);
 
+	// (diagnostics: 2048 skips the deferred packets, 4096 the counter
+	// flushes -- results wrong; the tail's phases measured by subtraction)
+	if (dg & 2048)
+		ndef = 0;
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
 		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
 		const bool ok = d0 + lane < ndef;
@@ -1167,12 +1171,14 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	__syncthreads();
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
-	cn.flush(a, tid, NT);
-	if constexpr (PORTS)
-		if (ptab)
-			for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
-				if (s_pcnt[i])
-					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
+	if (!(dg & 4096)) {
+		cn.flush(a, tid, NT);
+		if constexpr (PORTS)
+			if (ptab)
+				for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
+					if (s_pcnt[i])
+						atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
+	}
 	if (a.tlog && !(dg & 16))   // (win is free now: the partition scratch)
 		log_partition<NW>(a, s_tn, s_lh, win, tid);
 }
