@@ -3,7 +3,7 @@
 frames, xdpfilt_dny_all, 1M IPv4 rules (BASELINE.json configs[2] = "C3").
 
 One step = one xfg_classify() launch over the whole synthetic batch resident
-in HBM (2^24 packets of 64 B per GPU by default).  N GPUs = N processes, one
+in HBM (2^26 packets of 64 B, a 4 GiB batch, per GPU by default).  N GPUs = N processes, one
 per GPU, each with its own shard (rank-seeded batch; rule tables replicated):
 weak scaling, no data-path collective.  Counters are reduced over RCCL once,
 after the timed region (reported separately as reduce_ms).
@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log2-packets", type=int, default=24)
+    ap.add_argument("--log2-packets", type=int, default=26)
     ap.add_argument("--rules", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline duration (0 disables)")

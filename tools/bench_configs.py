@@ -32,7 +32,7 @@ def run(name, args):
     import xftools as X
     import xfgpu as G
     kind = {"c2": 2, "c4": 4, "c5": 5, "c3sd": 3}[name]
-    n = 1 << (args.log2_packets or {"c2": 24, "c4": 21, "c5": 20, "c3sd": 24}[name])
+    n = 1 << (args.log2_packets or {"c2": 24, "c4": 23, "c5": 23, "c3sd": 24}[name])
     stride = 64 if kind in (2, 3) else 1536
     n4 = {2: 1000, 3: 1_000_000, 4: 1_000_000, 5: 15_000_000}[kind]
     flag = 3 if name == "c3sd" else 2
