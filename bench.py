@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "xdp-tools_amd", "python"))
 
 METRIC = "Mpps classified (device-resident), 64B frames, xdpfilt_dny_all; 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0
+REDUCE_TIMEOUT_S = 120.0   # the readout all-reduce (outside the timed region)
 
 
 def parse():
@@ -43,6 +44,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline duration (0 disables)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank uses device 0 (RCCL then "
+                         "refuses the shared device, which the line reports as reduce_error)")
     ap.add_argument("--host-log2-packets", type=int, default=22,
                     help="sample for the PCIe-inclusive host-buffer rate (0 disables)")
     return ap.parse_args()
@@ -61,7 +65,8 @@ def main():
     import xftools as X
     import xfgpu as G
 
-    f, bufs, n, stride, lens, alg_bytes, v4, ports, gen_s = setup(args, rank, local)
+    f, bufs, n, stride, lens, alg_bytes, v4, ports, gen_s = setup(args, rank,
+                                                                  0 if args.one_device else local)
     d_data, d_lens, d_verd = bufs
 
     def barrier():
@@ -93,16 +98,32 @@ def main():
     assert int(st[:, 0].sum()) == n * (args.steps + args.warmup), st
 
     # ---- RCCL counter reduce (once, after the timed region)
-    reduce_ms = None
+    # (outside the timed region; a failure or a stall here is reported in the
+    # line and never keeps the line from being printed)
+    reduce_ms, reduce_err, reduce_stuck = None, None, False
     if world > 1:
+        import threading
         uid = [G.Filter.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        f.comm_init(world, rank, uid[0])
-        f.sync()
-        barrier()
-        tr = time.perf_counter()
-        f.comm_allreduce()
-        reduce_ms = (time.perf_counter() - tr) * 1e3
+        box = {}
+
+        def _reduce():
+            try:
+                f.comm_init(world, rank, uid[0])
+                f.sync()
+                tr = time.perf_counter()
+                f.comm_allreduce()
+                f.sync()
+                box["ms"] = (time.perf_counter() - tr) * 1e3
+            except Exception as e:  # reported, not fatal to the measurement
+                box["err"] = repr(e)
+
+        th = threading.Thread(target=_reduce, daemon=True)
+        th.start()
+        th.join(REDUCE_TIMEOUT_S)
+        reduce_stuck = th.is_alive()
+        reduce_ms = box.get("ms")
+        reduce_err = "timed out" if reduce_stuck else box.get("err")
 
     # ---- achievable streaming-read peak on this device (same 1 GiB buffer)
     peak_meas_ms = f.stream_read_timed(d_data.ptr, n * stride, 5)
@@ -196,10 +217,15 @@ def main():
     }
     if reduce_ms is not None:
         line["reduce_ms"] = round(reduce_ms, 3)
+    if reduce_err is not None:
+        line["reduce_error"] = reduce_err
     if host_path is not None:
         line["host_path"] = host_path
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if reduce_stuck:   # a stalled collective: do not wait on it in teardown
+        sys.stdout.flush()
+        os._exit(0)
     f.close()
     if dist is not None:
         dist.destroy_process_group()
