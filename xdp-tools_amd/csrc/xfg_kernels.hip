@@ -849,12 +849,28 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m)
 	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Global-address-space accesses to buffers the pipelined kernels use in
+// their loops.  Through a generic pointer the compiler emits FLAT
+// instructions, which also count against the LDS counter: every later
+// lgkmcnt(0) of the iteration (each LDS read the parse waits for) then waits
+// for the store's write acknowledgement as well -- a memory round trip per
+// iteration.  A global store counts only against vmcnt, where the next
+// iteration's one wait covers it.
+__device__ __forceinline__ void gst32(uint32_t *p, uint32_t v)
+{
+	*reinterpret_cast<__attribute__((address_space(1))) uint32_t *>((uintptr_t)p) = v;
+}
+__device__ __forceinline__ uint32_t gld32(const uint32_t *p)
+{
+	return *reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>((uintptr_t)p);
+}
+
 __device__ __forceinline__ void log_append(uint32_t *region, uint32_t &cnt, uint32_t tag, int lane)
 {
 	const unsigned long long m = __ballot(tag != CT_NONE);
 	if (m) {
 		if (tag != CT_NONE)
-			region[cnt + lanes_below(m)] = tag;
+			gst32(region + cnt + lanes_below(m), tag);
 		cnt += (uint32_t)__popcll(m);
 	}
 }
@@ -923,7 +939,7 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 #pragma unroll
 				for (int q = 1; q < NW; q++)
 					w += e >= pre[q];
-				g[j] = a.tlog[r0 + (uint64_t)w * a.defer_cap + (e - pre[w])];
+				g[j] = gld32(a.tlog + r0 + (uint64_t)w * a.defer_cap + (e - pre[w]));
 			}
 		}
 	};
@@ -972,7 +988,7 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 			if (a.diag & 256)   // diagnostics build only: no write-out
 				continue;
 			if (pos < a.pcap)
-				a.pbuf[(uint64_t)p * a.pcap + pos] = x;
+				gst32(a.pbuf + (uint64_t)p * a.pcap + pos, x);
 			else
 				atomicAdd(global_counter(a, x), 1ull);
 		}

@@ -541,7 +541,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 			if (dm) {
 				const uint32_t pos = ndef + lanes_below(dm);
 				if (w_act == A_DEFER)
-					dlist[pos] = gi;
+					gst32(dlist + pos, gi);
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
 		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
 		if (d0 + lane < ndef) {
-			const uint32_t gi = dlist[d0 + lane];
+			const uint32_t gi = gld32(dlist + d0 + lane);
 			len = min(load_len(a, gi), a.stride);
 			act = classify_one<FEAT>(a, s_ports, gi, len, tag);
 			__builtin_nontemporal_store((uint8_t)act, a.verdicts + gi);
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 			if (dm) {
 				const uint32_t pos = ndef + lanes_below(dm);
 				if (w_act == A_DEFER)
-					dlist[pos] = gi;
+					gst32(dlist + pos, gi);
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipe4_
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
 		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
 		const bool ok = d0 + lane < ndef;
-		const uint32_t gi = ok ? dlist[d0 + lane] : 0u;
+		const uint32_t gi = ok ? gld32(dlist + d0 + lane) : 0u;
 		if (ok)
 			len = min(load_len(a, gi), a.stride);
 #ifdef XFG_DIAG

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), 4) void xfg_look4_kernel(const xfg
 			if (dm) {
 				const uint32_t pos = ndef + lanes_below(dm);
 				if (w_act == A_DEFER)
-					dlist[pos] = gi;
+					gst32(dlist + pos, gi);
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), 4) void xfg_look4_kernel(const xfg
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
 		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
 		const bool ok = d0 + lane < ndef;
-		const uint32_t gi = ok ? dlist[d0 + lane] : 0u;
+		const uint32_t gi = ok ? gld32(dlist + d0 + lane) : 0u;
 		if (ok)
 			len = min(load_len(a, gi), a.stride);
 		act = classify_staged<FEAT, W>(a, s_ports, myrow, ok, gi, len, tag);
