@@ -882,7 +882,10 @@ __device__ __forceinline__ void log_append(uint32_t *region, uint32_t &cnt, uint
 // counting-sorted by partition in LDS and written out as per-partition runs
 // (consecutive lanes, consecutive addresses).  s: LDS scratch of
 // 4 * XFG_LOG_PARTS + LOG_CHUNK words.  Whole workgroup, after a barrier.
-constexpr uint32_t LOG_CHUNK = 8192;
+#ifndef XFG_LOG_CHUNK
+#define XFG_LOG_CHUNK 8192
+#endif
+constexpr uint32_t LOG_CHUNK = XFG_LOG_CHUNK;
 constexpr uint32_t LOG_SCRATCH = 4 * XFG_LOG_PARTS + LOG_CHUNK;   // words
 
 template <int NW>
