@@ -13,9 +13,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 min(len,128)+1) / average kernel duration from
                 HIP events on the launch stream, vs the 8 TB/s HBM peak
   cpu_baseline: the CPU restatement of xdpfilt_dny_all (oracle/, "port")
-                on a bounded sample of the same workload (N=1, rank 0 only),
-                on all the host cores this process may use and on one; the
-                CPU model is named.  The reference's own in-kernel run (C1) is
+                with the reference's cost model (one hash probe per
+                CHECK_MAP, per-thread counters summed) on a bounded sample
+                of the same workload (N=1, rank 0 only), on all the host
+                cores this process may use and on one; the CPU model is
+                named.  The reference's own in-kernel run (C1) is
                 not measured: it needs a BPF-capable clang, libbpf, bpffs,
                 veth/iproute2 and root, none of which this image has.
 """
@@ -49,18 +51,75 @@ def parse():
                          "refuses the shared device, which the line reports as reduce_error)")
     ap.add_argument("--host-log2-packets", type=int, default=22,
                     help="sample for the PCIe-inclusive host-buffer rate (0 disables)")
+    ap.add_argument("--rank-timeout", type=float, default=1800.0,
+                    help="self-launch (--gpus N without a launcher): seconds before the "
+                         "ranks count as stalled")
+    # launcher tests (CPU only): a rank body that touches no GPU
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` with no launcher around it (WORLD_SIZE unset): start N fresh
+    rank processes of this script -- RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT set, never exec, and before anything in this
+    process touches a GPU -- relay rank 0's line (the other ranks' stdout goes
+    to stderr), and return non-zero if any rank fails or the ranks stall past
+    --rank-timeout (each rank is then killed by its own process group)."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=None if r == 0 else 2,
+                                      start_new_session=True))
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+        for p in procs:
+            p.wait()
+
+    deadline = time.monotonic() + args.rank_timeout
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            print(f"bench: a rank failed (exit {bad[0]}); stopping the others", file=sys.stderr)
+            kill_all()
+            return bad[0] if bad[0] > 0 else 1
+        if all(c == 0 for c in codes):
+            return 0
+        if time.monotonic() > deadline:
+            print(f"bench: ranks stalled past {args.rank_timeout:.0f}s; killed", file=sys.stderr)
+            kill_all()
+            return 124
+        time.sleep(0.1)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.stub:
+        sys.exit(stub_rank(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # gloo: CPU barrier/max only
-        dist.init_process_group("gloo")
+    dist = init_gloo() if world > 1 else None   # gloo: CPU barriers / max only
     import numpy as np
     import xftools as X
     import xfgpu as G
@@ -87,11 +146,7 @@ def main():
     f.sync()
     barrier()
     wall = time.perf_counter() - t1
-    if dist is not None:
-        import torch
-        t = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = max_over_ranks(dist, wall)
 
     # ---- sanity on the run's own outputs (cheap, not a parity claim)
     st = f.stats(dev=0)
@@ -225,10 +280,61 @@ def main():
         print(json.dumps(line), flush=True)
     if reduce_stuck:   # a stalled collective: do not wait on it in teardown
         sys.stdout.flush()
-        os._exit(0)
+        os._exit(3)
     f.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def init_gloo():
+    """The CPU process group (barriers, the max over ranks); gloo's connect
+    message goes to stderr, so that stdout carries only the JSON line."""
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+    return dist
+
+
+def max_over_ranks(dist, wall):
+    """The timed region's wall time, max over ranks (gloo; CPU tensor)."""
+    if dist is None:
+        return wall
+    import torch
+    t = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def stub_rank(args):
+    """Launcher test body (no GPU): the rank's barriers and max-over-ranks
+    wall time over gloo, and rank 0's line with n_gpus = world size."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == args.stub_fail_rank:
+        return 3
+    dist = init_gloo() if world > 1 else None
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    if dist is not None:
+        dist.barrier()
+    wall = max_over_ranks(dist, time.perf_counter() - t1)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "Mpps", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(wall * 1e3 / max(args.steps, 1), 4),
+                          "stub": True}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
 
 
 def setup(args, rank, local):
@@ -290,9 +396,14 @@ def host_threads():
 
 
 def cpu_baseline(X, np, v4, ports, seconds):
-    """The C restatement of xdpfilt_dny_all (oracle/xf_oracle.c, "port") over
-    a 2^22-packet sample of the same workload (1M IPv4 rules), repeated until
-    ~`seconds` elapsed: on every usable host core (`value`) and on one."""
+    """The reference's CPU cost model on a 2^22-packet sample of the same C3
+    workload (1M IPv4 rules): the C restatement of xdpfilt_dny_all with a
+    hash index probed once per CHECK_MAP (BPF_MAP_TYPE_PERCPU_HASH,
+    xdp-filter/xdpfilt_prog.h:56-64) and per-thread counters summed at the
+    end, as per-CPU maps are (xdp-filter/xdp-filter.c:93-103) -- on every
+    usable host core (`value`) and on one.  The parity checker's own rate
+    (binary search over the sorted rules) is reported as `oracle_rate`
+    only."""
     m = 1 << 22
     stride = 64
     buf = np.zeros(m * stride, np.uint8)
@@ -304,10 +415,10 @@ def cpu_baseline(X, np, v4, ports, seconds):
     for p in ports:
         rules.ports[X.port_key(int(p))] = 2 | 4 | 8
     rules = rules.prepared()
-    maps = X.OracleMaps(rules)
+    hmaps = X.OracleMaps(rules, hashed=True)
     feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
 
-    def rate(threads, secs):
+    def rate(threads, secs, maps):
         done, t0 = 0, time.perf_counter()
         while True:
             X.run_oracle(feats, buf, lens, rules, stride=stride, maps=maps, nthreads=threads)
@@ -316,13 +427,19 @@ def cpu_baseline(X, np, v4, ports, seconds):
             if el >= secs:
                 return done, el
     nt = host_threads()
-    d1, e1 = rate(1, seconds / 2)
-    dn, en = rate(nt, seconds / 2)
+    d1, e1 = rate(1, seconds * 0.4, hmaps)
+    dn, en = rate(nt, seconds * 0.4, hmaps)
+    do, eo = rate(1, seconds * 0.2, X.OracleMaps(rules))
     return {"value": round(dn / en / 1e6, 2), "unit": "Mpps", "cores": nt, "kind": "port",
             "value_1thread": round(d1 / e1 / 1e6, 2),
+            "model": "C restatement of xdpfilt_dny_all (oracle/xf_oracle.c) with one hash "
+                     "probe per CHECK_MAP (the BPF hash map's cost) and per-thread counters "
+                     "summed at the end (per-CPU maps)",
+            "oracle_rate_1thread": round(do / eo / 1e6, 2),
             "cpu_model": cpu_model(),
             "sample": f"2^22-packet C3 sample, 1M IPv4 rules: {dn // m} passes on {nt} threads "
-                      f"({en:.1f}s) and {d1 // m} on 1 thread ({e1:.1f}s); oracle restatement",
+                      f"({en:.1f}s), {d1 // m} on 1 thread ({e1:.1f}s); checker (binary "
+                      f"search) {do // m} on 1 thread ({eo:.1f}s)",
             "c1": "not measured: the in-kernel XDP/veth run needs a BPF-capable clang, libbpf, "
                   "bpffs, iproute2 and root, absent from this image"}
 

@@ -33,7 +33,55 @@ struct xfo_map {
 	uint32_t n, keylen;
 	const uint8_t *keys;
 	uint32_t *order; /* rule indices sorted by key bytes */
+	/* Optional hash index (xfo_map_new_hashed): open addressing, linear
+	 * probing, load <= 1/2; slot = fingerprint << 32 | flags << 26 |
+	 * (index + 1), 0 = empty, where flags is the rule's flag byte (low 6
+	 * bits of its value) when the index was built: one cache line answers
+	 * a miss and a flag mismatch, as the reference's hash element holds its
+	 * key and value together.  For 4-byte keys the fingerprint IS the key.
+	 * It gives the restatement the reference's cost model -- one hash probe
+	 * per CHECK_MAP (BPF_MAP_TYPE_PERCPU_HASH, xdp-filter/xdpfilt_prog.h:56-64)
+	 * -- for the CPU baseline; the binary search stays the checker's index. */
+	uint64_t *slots;
+	uint64_t smask;
 };
+
+static inline uint32_t fmix32(uint32_t h)
+{
+	h ^= h >> 16;
+	h *= 0x85ebca6bu;
+	h ^= h >> 13;
+	h *= 0xc2b2ae35u;
+	h ^= h >> 16;
+	return h;
+}
+
+static inline uint32_t key_hash(const uint8_t *k, uint32_t len)
+{
+	uint32_t h = 0x9747b28cu ^ len;
+	uint32_t i = 0;
+	for (; i + 4 <= len; i += 4) {
+		uint32_t w;
+		memcpy(&w, k + i, 4);
+		h = fmix32(h ^ w);
+	}
+	if (i < len) {
+		uint32_t w = 0;
+		memcpy(&w, k + i, len - i);
+		h = fmix32(h ^ w);
+	}
+	return h;
+}
+
+static inline uint32_t key_fp(const uint8_t *k, uint32_t len, uint32_t h)
+{
+	uint32_t w;
+	if (len == 4) {
+		memcpy(&w, k, 4);
+		return w;
+	}
+	return h;
+}
 
 static const uint8_t *g_sort_keys;
 static uint32_t g_sort_len;
@@ -72,10 +120,51 @@ xfo_map *xfo_map_new(uint32_t n, uint32_t keylen, const uint8_t *keys)
 	return m;
 }
 
+#define SLOT_IDX(e) ((uint32_t)((e) & ((1u << 26) - 1)) - 1)
+#define SLOT_FLAGS(e) ((uint32_t)((e) >> 26) & 63)
+
+xfo_map *xfo_map_new_hashed(uint32_t n, uint32_t keylen, const uint8_t *keys,
+			    const uint64_t *vals)
+{
+	if (n >= (1u << 26) - 1)
+		return NULL;
+	xfo_map *m = xfo_map_new(n, keylen, keys);
+	if (!m)
+		return NULL;
+	uint64_t cap = 16;
+	while (cap < 2ull * n)
+		cap <<= 1;
+	m->slots = calloc(cap, sizeof(uint64_t));
+	if (!m->slots) {
+		xfo_map_free(m);
+		return NULL;
+	}
+	m->smask = cap - 1;
+	for (uint32_t i = 0; i < n; i++) {   /* index order: the first occurrence wins */
+		const uint8_t *k = keys + (size_t)i * keylen;
+		const uint32_t h = key_hash(k, keylen), fp = key_fp(k, keylen, h);
+		uint64_t j = h & m->smask;
+		int dup = 0;
+		while (m->slots[j]) {
+			const uint64_t e = m->slots[j];
+			if ((uint32_t)(e >> 32) == fp &&
+			    !memcmp(keys + (size_t)SLOT_IDX(e) * keylen, k, keylen)) {
+				dup = 1;
+				break;
+			}
+			j = (j + 1) & m->smask;
+		}
+		if (!dup)
+			m->slots[j] = ((uint64_t)fp << 32) | ((uint64_t)(vals[i] & 63) << 26) | (i + 1u);
+	}
+	return m;
+}
+
 void xfo_map_free(xfo_map *m)
 {
 	if (m) {
 		free(m->order);
+		free(m->slots);
 		free(m);
 	}
 }
@@ -112,8 +201,34 @@ struct run_state {
 
 /* CHECK_MAP, xdp-filter/xdpfilt_prog.h:56-64: hit iff the key exists and
  * (value & mask) == mask; a hit adds 1 << COUNTER_SHIFT to that value. */
+/* The hashed index's probe: the slot of @key, or 0. */
+static inline uint64_t hash_probe(const xfo_map *m, const uint8_t *key)
+{
+	const uint32_t h = key_hash(key, m->keylen), fp = key_fp(key, m->keylen, h);
+	for (uint64_t j = h & m->smask;; j = (j + 1) & m->smask) {
+		const uint64_t e = m->slots[j];
+		if (!e || ((uint32_t)(e >> 32) == fp &&
+			   (m->keylen == 4 || !memcmp(m->keys + (size_t)SLOT_IDX(e) * m->keylen, key, m->keylen))))
+			return e;
+	}
+}
+
 static inline int check_hash(const xfo_map *m, uint64_t *vals, const uint8_t *key, uint32_t mask)
 {
+	if (m && m->slots) {
+		/* one probe; the rule's value is touched only when its flags
+		 * (as indexed) carry the mask -- then it is the authority */
+		if (!m->n)
+			return 0;
+		const uint64_t e = hash_probe(m, key);
+		if (!e || (SLOT_FLAGS(e) & mask) != mask)
+			return 0;
+		const uint32_t i = SLOT_IDX(e);
+		if ((vals[i] & mask) != mask)
+			return 0;
+		vals[i] += 1u << 6;
+		return 1;
+	}
 	int64_t i = map_find(m, key);
 	if (i >= 0 && (vals[i] & mask) == mask) {
 		vals[i] += 1u << 6;

@@ -188,6 +188,8 @@ def oracle():
         lib = C.CDLL(os.path.join(ROOT, "oracle", "build-asan" if _ASAN else "build", "liboracle.so"))
         lib.xfo_map_new.restype = C.c_void_p
         lib.xfo_map_new.argtypes = [C.c_uint32, C.c_uint32, _u8p]
+        lib.xfo_map_new_hashed.restype = C.c_void_p
+        lib.xfo_map_new_hashed.argtypes = [C.c_uint32, C.c_uint32, _u8p, _u64p]
         lib.xfo_map_free.argtypes = [C.c_void_p]
         common = [C.c_uint32, _u8p, _u64p, C.c_uint32, C.c_void_p, C.c_int, C.c_uint64, _u64p]
         lib.xfo_run.argtypes = common + [C.c_void_p, _u64p, C.c_void_p, _u64p, C.c_void_p,
@@ -202,13 +204,21 @@ def oracle():
 class OracleMaps:
     """Prebuilt exact-match indexes for a RuleSet (reusable across runs)."""
 
-    def __init__(self, rules: RuleSet):
+    def __init__(self, rules: RuleSet, hashed: bool = False):
+        """hashed: add the hash index (one probe per lookup, the reference's
+        BPF hash-map cost model: the CPU baseline); results are identical."""
         lib = oracle()
         self.rules = rules.prepared()
         r = self.rules
-        self.m4 = lib.xfo_map_new(len(r.v4_keys), 4, ptr(r.v4_keys))
-        self.m6 = lib.xfo_map_new(len(r.v6_keys), 16, ptr(r.v6_keys))
-        self.me = lib.xfo_map_new(len(r.eth_keys), 6, ptr(r.eth_keys))
+        if hashed:   # (the slots carry the rules' flags as they are now)
+            self.m4 = lib.xfo_map_new_hashed(len(r.v4_keys), 4, ptr(r.v4_keys), ptr(r.v4_vals, _u64p))
+            self.m6 = lib.xfo_map_new_hashed(len(r.v6_keys), 16, ptr(r.v6_keys), ptr(r.v6_vals, _u64p))
+            self.me = lib.xfo_map_new_hashed(len(r.eth_keys), 6, ptr(r.eth_keys),
+                                             ptr(r.eth_vals, _u64p))
+        else:
+            self.m4 = lib.xfo_map_new(len(r.v4_keys), 4, ptr(r.v4_keys))
+            self.m6 = lib.xfo_map_new(len(r.v6_keys), 16, ptr(r.v6_keys))
+            self.me = lib.xfo_map_new(len(r.eth_keys), 6, ptr(r.eth_keys))
 
     def __del__(self):
         try:

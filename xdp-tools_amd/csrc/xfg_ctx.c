@@ -1049,7 +1049,19 @@ int xfg_map_update_batch_percpu(xfg_ctx *ctx, int map, const void *keys, const u
  * table (linear probing from xfg_port_slot()) when at most XFG_PORT_TAB_MAX
  * ports carry flags, else the nibble map of every port's low 4 flag bits
  * (the only ones CHECK_MAP can test). */
+static int port_tab_refresh_locked(struct xfg_dev *d);
+
 static int port_tab_refresh(struct xfg_dev *d)
+{
+	/* (under the device lock: launch_batch reads the image's kind and
+	 * displacement there; lock order ctx->lock, then d->lock) */
+	pthread_mutex_lock(&d->lock);
+	int err = port_tab_refresh_locked(d);
+	pthread_mutex_unlock(&d->lock);
+	return err;
+}
+
+static int port_tab_refresh_locked(struct xfg_dev *d)
 {
 	uint32_t tab[XFG_PORT_TAB];
 	uint32_t n = 0, disp = 0;
@@ -1201,6 +1213,12 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.dcnt = a.gbase[3];       /* every hash-map counter */
 	else if (a.gbase[1] <= XFG_DCNT_MAX)
 		a.dcnt = a.gbase[1];       /* the IPv4 map's counters */
+	pthread_mutex_lock(&d->lock);
+	/* the port image in stream order at this launch (another caller's
+	 * port_tab_refresh may have rewritten it since fill_kargs; both hold
+	 * d->lock for that): its kind and its longest displacement */
+	a.port_tab = d->port_tab_ok ? d->port_tab : NULL;
+	a.port_tab_disp = d->port_tab_disp;
 	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
 #ifdef XFG_DIAG
 	const char *g = getenv("XFG_GRID_PER_CU");
@@ -1221,7 +1239,6 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.grid_parse = (uint32_t)(gp < np ? gp : (np ? np : 1));
 	}
 
-	pthread_mutex_lock(&d->lock);
 	if (a.split) {
 		/* parse-pass records: key a, ports, key b (both directions live) */
 		int both = a.t4.count && (a.t4.fmask & 3) == 3;
@@ -1257,7 +1274,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			goto out;
 		if (!d->pfill) {
 			if ((err = hip_err(hipMalloc((void **)&d->pfill, XFG_LOG_PARTS * 4))) ||
-			    (err = hip_err(hipMemset(d->pfill, 0, XFG_LOG_PARTS * 4))))
+			    (err = hip_err(hipMemsetAsync(d->pfill, 0, XFG_LOG_PARTS * 4, d->stream))))
 				goto out;
 		}
 		a.tlog = d->tlog;
@@ -1498,7 +1515,12 @@ static inline uint32_t hsrc_len(const struct hsrc *s, uint64_t i)
 {
 	if (s->descs)   /* xdp_desc.len: the low half of the record's second word */
 		return (uint32_t)s->descs[2ull * ((s->first + (uint32_t)i) & s->mask) + 1];
-	return s->lens_u16 ? ((const uint16_t *)s->lens)[i] : ((const uint32_t *)s->lens)[i];
+	const uint32_t l = s->lens_u16 ? ((const uint16_t *)s->lens)[i] : ((const uint32_t *)s->lens)[i];
+	/* a fixed-stride frame lies in its slot: a longer length is capped at the
+	 * slot, as the device path caps it (the gather, the kernel and the
+	 * whole-frame fallback then all see the same length, and no copy reads
+	 * past the slot) */
+	return (!s->offsets && s->stride && l > s->stride) ? s->stride : l;
 }
 
 struct gather_job {
@@ -1749,6 +1771,13 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 	const uint32_t stride = whole ? src->stride : HOST_WIN;
 	/* whole slots in a registered buffer: copied by DMA where they lie */
 	const int direct = whole && host_registered(ctx, src->data, n * (uint64_t)stride);
+	/* windows of larger slots in a registered buffer: one strided DMA per
+	 * chunk (rows of HOST_WIN bytes at the batch's stride; a window never
+	 * leaves its slot) instead of the pool's gather -- the pool then
+	 * gathers the lengths only */
+	const int direct2d = !whole && !src->descs && !src->offsets && src->stride > HOST_WIN &&
+			     !(src->stride & 15) &&
+			     host_registered(ctx, src->data, n * (uint64_t)src->stride);
 	uint64_t pend[2] = { UINT64_MAX, UINT64_MAX };   /* each slot's last chunk */
 
 	pthread_mutex_lock(&d->host_lock);
@@ -1761,11 +1790,15 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 		if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
 			goto fail;
 		struct gather_job job = { src, c, m, d->hs_hbuf[k], d->hs_hl[k], stride, whole && !direct };
-		if (direct)   /* (the slots go by DMA: only the lengths are gathered) */
+		if (direct || direct2d)   /* (the slots go by DMA: only the lengths are gathered) */
 			job.whole = 2;
 		hpool_run(d->pool, gather_slice, &job);
-		HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], direct ? src->data + c * stride : d->hs_hbuf[k],
-				      m * stride, hipMemcpyHostToDevice, d->hs_st[k]));
+		if (direct2d)
+			HIPCHK(hipMemcpy2DAsync(d->hs_dbuf[k], HOST_WIN, src->data + c * src->stride,
+						src->stride, HOST_WIN, m, hipMemcpyHostToDevice, d->hs_st[k]));
+		else
+			HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], direct ? src->data + c * stride : d->hs_hbuf[k],
+					      m * stride, hipMemcpyHostToDevice, d->hs_st[k]));
 		HIPCHK(hipMemcpyAsync(d->hs_dl[k], d->hs_hl[k], m * 4, hipMemcpyHostToDevice, d->hs_st[k]));
 		HIPCHK(hipMemsetAsync(d->hs_fbc[k], 0, 4, d->hs_st[k]));
 		struct xfg_batch sub = { d->hs_dbuf[k], NULL, d->hs_dl[k], m, stride, 0 };
