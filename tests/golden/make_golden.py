@@ -14,9 +14,11 @@ Provenance: round 1 generated these same arrays from the reference's
 xdpfilt_*.c compiled for the host against stand-in BPF headers; such a build
 is not a reference build by this project's rules (the reference needs
 libbpf's headers and the kernel's map runtime, absent here: DESIGN.md §2),
-so it was removed and the fixture is now what the restatement produces --
-byte-identical to the round-1 file.  It pins regressions of the restatement
-and of the HIP path; the reference-held expectations are tests/kat.py's rows.
+so it was removed and the fixture is now what the restatement produces
+(byte-identical to the round-1 file until round 3 added the reference-traffic
+rows Q1-Q20 to tests/kat.py).  It is RESTATEMENT-DERIVED: it pins regressions
+of the restatement and of the HIP path, not parity with the reference; the
+reference-held expectations are tests/kat.py's rows.
 """
 import os
 import sys

@@ -35,6 +35,22 @@ SRC, DST, TCPF, UDPF = 1, 2, 4, 8
 A_SRC, A_DST = "192.0.2.1", "192.0.2.2"
 A6_SRC, A6_DST = "2001:db8::1", "2001:db8::2"
 
+# The reference test bed (lib/testing/test_runner.sh:361-397): the program
+# runs on the OUTSIDE end of a veth pair and sees what the namespace's INSIDE
+# end sends; OUTSIDE = <prefix>1, INSIDE = <prefix>2 in 10.11.<n>.0/24 and
+# fc42:dead:cafe:<n>::/64.  Each test function loads its own rules; here the
+# rows share one rule set, so each phase gets its own <n>: 2 = a dst rule on
+# OUTSIDE (`xdp-filter ip $OUTSIDE_IP*`), 4 = a src rule on INSIDE (`ip -m src
+# $INSIDE_IP*`), 3 = no address rule (the port tests).
+OUT4, IN4 = "10.11.2.1", "10.11.2.2"
+OUT4_S, IN4_SRC = "10.11.4.1", "10.11.4.2"
+OUT6, IN6 = "fc42:dead:cafe:2::1", "fc42:dead:cafe:2::2"
+OUT6_S, IN6_SRC = "fc42:dead:cafe:4::1", "fc42:dead:cafe:4::2"
+OUT6_N, IN6_N = "fc42:dead:cafe:3::1", "fc42:dead:cafe:3::2"
+OUT4_N, IN4_N = "10.11.3.1", "10.11.3.2"
+OUT_MAC, IN_MAC = "02:00:00:00:02:01", "02:00:00:00:02:02"
+OUT_MAC_S, IN_MAC_SRC = "02:00:00:00:04:01", "02:00:00:00:04:02"
+
 
 def port_key(p):
     return ((p & 0xff) << 8) | (p >> 8)
@@ -48,17 +64,24 @@ def kat_rules():
     rs.ports[port_key(2000)] = SRC | TCPF         # tcp source-port rule
     rs.ports[port_key(3000)] = DST | UDPF         # udp only: TCP to 3000 misses
     rs.ports[port_key(4000)] = SRC | DST | UDPF | TCPF
+    # the reference tests' `xdp-filter port N` (default mode dst, tcp|udp,
+    # xdp-filter/xdp-filter.c:647-651) and test_basic.py's default-packet ports
+    rs.ports[port_key(10000)] = DST | TCPF | UDPF
+    rs.ports[port_key(60002)] = DST | TCPF | UDPF
+    rs.ports[port_key(60001)] = SRC | TCPF | UDPF
     v4 = [("10.0.0.1", SRC), ("10.11.1.2", DST), ("10.11.1.9", SRC | DST),
-          ("10.22.0.1", SRC), ("10.33.0.1", DST), ("0.0.0.0", DST)]
+          ("10.22.0.1", SRC), ("10.33.0.1", DST), ("0.0.0.0", DST),
+          (OUT4, DST), (IN4_SRC, SRC)]
     rs.v4_keys = np.array([list(P.ip4(a)) for a, _ in v4], np.uint8)
     rs.v4_vals = np.array([f | (7 << 6) for _, f in v4], np.uint64)   # pre-existing hits
     v6 = [("fc00:dead:cafe:1::2", DST), ("fc00:dead:cafe:1::1", SRC),
           ("fc00::99", SRC | DST), ("::ffff:10.11.1.1", SRC), ("fe80::1", DST),
-          ("fe80::2", SRC), ("::", SRC)]
+          ("fe80::2", SRC), ("::", SRC), (OUT6, DST), (IN6_SRC, SRC)]
     rs.v6_keys = np.array([list(P.ip6(a)) for a, _ in v6], np.uint8)
     rs.v6_vals = np.array([f for _, f in v6], np.uint64)
     macs = [("aa:00:00:00:00:01", DST), ("aa:00:00:00:00:02", SRC),
-            ("aa:00:00:00:00:03", SRC | DST), ("00:00:00:00:00:00", SRC)]
+            ("aa:00:00:00:00:03", SRC | DST), ("00:00:00:00:00:00", SRC),
+            (OUT_MAC, DST), (IN_MAC_SRC, SRC)]
     rs.eth_keys = np.array([list(P.mac(m)) for m, _ in macs], np.uint8)
     rs.eth_vals = np.array([f for _, f in macs], np.uint64)
     return rs
@@ -239,4 +262,64 @@ def kat_frames():
     add("L2 exactly eth header", P.eth(), dny_all=ABORTED, dny_eth=DROP)
     add("L3 ipv4 exactly 20B hdr, proto 17, no udp", P.eth() + P.ipv4(A_SRC, A_DST, 17),
         dny_all=ABORTED, dny_ip=DROP)
+
+    # ---- the reference tests' traffic, as their tools put it on the wire ----
+    # (test-xdp-filter.sh: socat TCP6/UDP6 :89-90, ping6 :134, ndisc6 :139,
+    # ping :178, arping :183, arping -A :188; test_basic.py's default packets)
+    e6 = P.eth(ethertype=0x86DD)
+    add("Q1 socat TCP6 SYN (doff 10) to port 10000", Ann(hit=("port", 10000), src=SH + ":89"),
+        e6 + P.ipv6(IN6_N, OUT6_N, 6, P.tcp_syn_linux(40000, 10000)),
+        dny_tcp=PASS, alw_tcp=DROP, dny_all=PASS, alw_all=DROP, dny_udp=DROP, dny_ip=DROP)
+    add("Q2 socat TCP6 SYN (doff 10) to port 10001", Ann(src=SH + ":89"),
+        e6 + P.ipv6(IN6_N, OUT6_N, 6, P.tcp_syn_linux(40000, 10001)),
+        dny_tcp=DROP, alw_tcp=PASS, dny_all=DROP, alw_all=PASS)
+    add("Q3 socat UDP6 'test' to port 10000", Ann(hit=("port", 10000), src=SH + ":90"),
+        e6 + P.ipv6(IN6_N, OUT6_N, 17, P.udp(40001, 10000, b"test\n")),
+        dny_udp=PASS, alw_udp=DROP, dny_all=PASS, alw_all=DROP, dny_tcp=DROP, dny_ip=DROP)
+    add("Q4 socat UDP6 'test' to port 10001", Ann(src=SH + ":90"),
+        e6 + P.ipv6(IN6_N, OUT6_N, 17, P.udp(40001, 10001, b"test\n")),
+        dny_udp=DROP, alw_udp=PASS, dny_all=DROP)
+    add("Q5 socat TCP4-style SYN (doff 10) to port 10000", Ann(hit=("port", 10000), src=SH + ":89"),
+        P.eth() + P.ipv4(IN4_N, OUT4_N, 6, payload=P.tcp_syn_linux(40000, 10000)),
+        dny_tcp=PASS, alw_tcp=DROP, dny_all=PASS)
+    add("Q6 ping to OUTSIDE (dst rule)", Ann(hit=("v4", OUT4), src=IPV4_SH.split(":")[0] + ":178"),
+        P.ping4(IN4, OUT4), dny_ip=PASS, alw_ip=DROP, dny_all=PASS, alw_all=DROP, dny_udp=DROP,
+        alw_tcp=PASS, alw_eth=PASS)
+    add("Q7 ping from INSIDE (src rule)", Ann(hit=("v4", IN4_SRC), src=IPV4_SH.split(":")[0] + ":178"),
+        P.ping4(IN4_SRC, OUT4_S), dny_ip=PASS, alw_ip=DROP, dny_all=PASS)
+    add("Q8 arping request for OUTSIDE (tip as DST)", Ann(hit=("v4", OUT4), src=SH + ":183"),
+        P.arping(1, P.mac(IN_MAC), IN4, OUT4), dny_ip=PASS, alw_ip=DROP, dny_all=PASS,
+        dny_udp=DROP, alw_eth=PASS)
+    add("Q9 arping -A from INSIDE (reply, sip = tip, src rule)", Ann(hit=("v4", IN4_SRC), src=SH + ":188"),
+        P.arping(2, P.mac(IN_MAC), IN4_SRC, IN4_SRC), dny_ip=PASS, alw_ip=DROP, dny_all=PASS)
+    add("Q10 arping -A with no src rule", Ann(src=SH + ":188"),
+        P.arping(2, P.mac(IN_MAC), IN4, IN4), dny_ip=DROP, alw_ip=PASS)
+    add("Q11 ping6 to OUTSIDE (dst rule)", Ann(hit=("v6", OUT6), src=SH + ":134"),
+        P.ping6(IN6, OUT6), dny_ip=PASS, alw_ip=DROP, dny_all=PASS, dny_udp=DROP)
+    add("Q12 ping6 from INSIDE (src rule)", Ann(hit=("v6", IN6_SRC), src=SH + ":134"),
+        P.ping6(IN6_SRC, OUT6_S), dny_ip=PASS, alw_ip=DROP)
+    add("Q13 ndisc6 NS for OUTSIDE, SLLA option (target as DST)", Ann(hit=("v6", OUT6), src=SH + ":139"),
+        P.ndisc6_ns(IN6, OUT6, P.mac(IN_MAC)), dny_ip=PASS, alw_ip=DROP, dny_all=PASS,
+        dny_udp=DROP, dny_tcp=DROP)
+    add("Q14 ndisc6 NS for an unruled target", Ann(src=SH + ":139"),
+        P.ndisc6_ns(IN6_N, OUT6_N, P.mac(IN_MAC)), dny_ip=DROP, alw_ip=PASS)
+    add("Q15 ping6 to OUTSIDE_MAC (ether dst rule)", Ann(hit=("eth", OUT_MAC), src=ETHER_SH),
+        P.ping6(IN6_N, OUT6_N, P.eth(dst=P.mac(OUT_MAC), src=P.mac(IN_MAC), ethertype=0x86DD)),
+        dny_eth=PASS, alw_eth=DROP, dny_all=PASS, dny_ip=DROP)
+    add("Q16 ping6 from INSIDE_MAC (ether src rule)", Ann(hit=("eth", IN_MAC_SRC), src=ETHER_SH),
+        P.ping6(IN6_N, OUT6_N, P.eth(dst=P.mac(OUT_MAC_S), src=P.mac(IN_MAC_SRC), ethertype=0x86DD)),
+        dny_eth=PASS, alw_eth=DROP, dny_all=PASS)
+    TB = "xdp-filter/tests/test_basic.py:88-92 (common.py:25-31 packets)"
+    add("Q17 default udp 60001->60002, `port 60002` (dst)", Ann(hit=("port", 60002), src=TB),
+        P.eth() + P.ipv4(IN4_N, OUT4_N, 17, payload=P.udp(60001, 60002)),
+        dny_udp=PASS, alw_udp=DROP, dny_all=PASS, alw_all=DROP, dny_ip=DROP)
+    add("Q18 default udp6 60001->60002, `port 60002` (dst)", Ann(hit=("port", 60002), src=TB),
+        e6 + P.ipv6(IN6_N, OUT6_N, 17, P.udp(60001, 60002)),
+        dny_udp=PASS, alw_udp=DROP, dny_all=PASS)
+    add("Q19 udp 60001->60005, `port 60001 --mode src`", Ann(hit=("port", 60001), src=TB),
+        P.eth() + P.ipv4(IN4_N, OUT4_N, 17, payload=P.udp(60001, 60005)),
+        dny_udp=PASS, alw_udp=DROP, dny_all=PASS)
+    add("Q20 tcp 60001->60005, `port 60001 --mode src`", Ann(hit=("port", 60001), src=TB),
+        P.eth() + P.ipv4(IN4_N, OUT4_N, 6, payload=P.tcp(60001, 60005)),
+        dny_tcp=PASS, alw_tcp=DROP, dny_udp=DROP)
     return F

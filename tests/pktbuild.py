@@ -80,3 +80,49 @@ def arp(op=1, sha=MAC_A, sip="10.11.1.1", tha=b"\x00" * 6, tip="10.11.1.2",
 
 def icmp4_echo() -> bytes:
     return struct.pack("!BBHHH", 8, 0, 0, 1, 1) + b"ping" * 4
+
+
+# ---- the shapes the reference's own test traffic has (iputils ping/ping6/
+# arping, socat, ndisc6), used by tests/kat.py's reference-traffic rows
+
+def ping_data() -> bytes:
+    """ping's default 56 data bytes: a 16-byte timestamp, then 0x10, 0x11, ..."""
+    return b"\x11" * 16 + bytes(range(0x10, 0x10 + 40))
+
+
+def ping4(src, dst, eth_hdr=None) -> bytes:
+    """`ping -c 1`: ICMP echo request, 64 ICMP bytes, DF, TTL 64 (98-byte frame)."""
+    icmp = struct.pack("!BBHHH", 8, 0, 0, 0x1234, 1) + ping_data()
+    return (eth_hdr or eth()) + ipv4(src, dst, 1, payload=icmp, frag=0x4000)
+
+
+def ping6(src, dst, eth_hdr=None) -> bytes:
+    """`ping6 -c 1`: ICMPv6 echo request, 64 ICMPv6 bytes (118-byte frame)."""
+    icmp = struct.pack("!BBHHH", 128, 0, 0, 0x1234, 1) + ping_data()
+    return (eth_hdr or eth(ethertype=0x86DD)) + ipv6(src, dst, 58, icmp)
+
+
+def tcp_syn_linux(sport, dport) -> bytes:
+    """A Linux connect() SYN (socat TCP6:...): doff 10, options MSS, SACK-permitted,
+    timestamps, NOP, window scale."""
+    opts = bytes.fromhex("020405a0" "0402" "080a") + struct.pack("!II", 0x01020304, 0) + \
+        bytes.fromhex("01" "030307")
+    return struct.pack("!HHIIBBHHH", sport, dport, 0x11223344, 0, 10 << 4, 0x02, 64800, 0, 0) + opts
+
+
+def arping(op, sha, sip, tip, tha=b"\xff" * 6) -> bytes:
+    """iputils arping: a 42-byte ARP frame to the broadcast address (`-A`: an ARP
+    reply with sip == tip)."""
+    return eth(dst=b"\xff" * 6, src=sha, ethertype=0x0806) + arp(op, sha=sha, sip=sip, tha=tha, tip=tip)
+
+
+def ndisc6_ns(src, target, sll) -> bytes:
+    """`ndisc6 -r 1 <target> -s <src> <if>`: a neighbour solicitation to the
+    target's solicited-node group, hop limit 255, with a source link-layer
+    address option (type 1, length 1)."""
+    t = ipaddress.IPv6Address(target).packed
+    group = ipaddress.IPv6Address("ff02::1:ff00:0").packed[:13] + t[13:]
+    body = struct.pack("!BBHI", 135, 0, 0, 0) + t + bytes([1, 1]) + sll
+    e = eth(dst=b"\x33\x33" + group[12:], src=sll, ethertype=0x86DD)
+    h = struct.pack("!IHBB16s16s", 0x60000000, len(body), 58, 255, ip6(src), group)
+    return e + h + body

@@ -1,0 +1,84 @@
+"""GPU parity at the bench's own batch size (SURVEY.md §8d's C3, as bench.py
+runs it): everything sized by the batch -- the hit-log partition buffers
+(2 n / 256 + 1024 entries each, spilling to atomics past that,
+xfg_ctx.c launch_batch), the per-wave deferred lists and hit-log regions,
+the count kernel -- is checked against the CPU restatement (oracle/) on
+every host thread, bit-exact: verdicts, all 1M rule values, per-action
+stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
+
+  * C3 at 2^26 packets, 16-bit lengths: bench.py's rank-0 shard exactly;
+  * a skewed C3 at 2^25: every hit on one of 8 hot rules, so each hot
+    rule's hits alone (~1.9M) overfill its hit-log partition (~263k
+    entries): the spill-to-atomics path runs at scale.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import xftools as X
+from test_gpu import assert_same, gpu_values, make_filter
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def G():
+    import xfgpu
+    return xfgpu
+
+
+def _threads():
+    t = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        t = min(t, int(omp))
+    return max(1, min(t, 16))
+
+
+def _c3_rules():
+    # bench.py setup(): 1M IPv4 dst rules (seed 3) + 16 dst|tcp|udp ports
+    v4 = X.rand_keys(3, int(1_000_000 * 1.02) + 16, 4)[:1_000_000]
+    ports = (np.arange(16, dtype=np.uint16) * 1031 + 53).astype(np.uint16)
+    rules = X.RuleSet()
+    rules.v4_keys = v4
+    rules.v4_vals = np.full(len(v4), 2, np.uint64)
+    for p in ports:
+        rules.ports[X.port_key(int(p))] = 2 | 4 | 8
+    return rules, v4, ports
+
+
+def _check(G, rules, data, lens):
+    ov, orules, ost = X.run_oracle(X.VARIANT_FEATURES["xdpfilt_dny_all"], data, lens, rules,
+                                   stride=64, nthreads=_threads())
+    f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=1_000_000)
+    f.load_rules(rules)
+    v = f.run(data, lens, stride=64)
+    assert_same(v, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
+    f.close()
+    return ov, orules
+
+
+@pytest.mark.timeout(900)
+def test_c3_at_bench_batch_2p26(G):
+    rules, v4, ports = _c3_rules()
+    n = 1 << 26
+    data, lens = X.gen_workload(3, 3, n, 64, v4=v4, ports=ports, dst_permille=500,
+                                port_permille=250, bad_permille=10)
+    ov, _ = _check(G, rules, data, lens.astype(np.uint16))
+    assert (ov == 2).sum() > n // 3          # the hits PASS under deny
+    assert (ov == 0).sum() > n // 1000       # malformed frames ABORT
+
+
+@pytest.mark.timeout(900)
+def test_c3_skewed_hits_overfill_log_partitions_2p25(G):
+    rules, v4, ports = _c3_rules()
+    n = 1 << 25
+    hot = v4[:8]
+    data, lens = X.gen_workload(33, 3, n, 64, v4=hot, ports=ports, dst_permille=500,
+                                port_permille=250, bad_permille=10)
+    _, orules = _check(G, rules, data, lens.astype(np.uint16))
+    pcap = 2 * ((n + 255) // 256) + 1024
+    hits = orules.v4_vals[:8] >> 6
+    assert (hits > pcap).all(), (hits, pcap)   # each hot rule alone overfills a partition
+    assert int((orules.v4_vals[8:] >> 6).sum()) == 0
