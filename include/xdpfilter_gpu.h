@@ -83,6 +83,11 @@ struct xfg_open_opts {
 	uint32_t ipv6_capacity;
 	uint32_t eth_capacity;
 	uint32_t hash_seed;      /* 0 => fixed default seed */
+	/* IPv4 maps with at least this many keys are looked up through the
+	 * one-read quotient index when it applies (fixed-stride batches, one
+	 * live IPv4 lookup direction, the same flags on every device): 0 =>
+	 * default (2^18), UINT32_MAX => never.  Results never depend on it. */
+	uint32_t qt_min_keys;
 };
 
 /*
@@ -102,6 +107,17 @@ const char *xfg_prog_name(const xfg_ctx *ctx);      /* e.g. "xdpfilt_dny_all" */
 uint32_t xfg_prog_features(const xfg_ctx *ctx);     /* the program's _features word */
 int xfg_num_devices(const xfg_ctx *ctx);            /* analogue of libbpf_num_possible_cpus() */
 const char *xfg_strerror(int err);
+
+/* The classify kernel the last launch on device @dev ran (introspection for
+ * tests and tools): XFG_PATH_GENERAL (offsets, descriptors, header
+ * windows), _PIPELINE (fixed stride, any live key), _IPV4 (IPv4 keys only:
+ * prefilter + bucket line), _QT (IPv4 keys only: the quotient index); or
+ * -EINVAL / -ENOENT (no launch yet). */
+#define XFG_PATH_GENERAL  0
+#define XFG_PATH_PIPELINE 1
+#define XFG_PATH_IPV4     2
+#define XFG_PATH_QT       5
+int xfg_last_path(const xfg_ctx *ctx, int dev);
 
 /*
  * Map operations.  As with a BPF per-CPU map, a value is one u64 per device

@@ -1,7 +1,9 @@
 """GPU parity tests: the HIP path (libxdpfilter_gpu.so on an MI355X) against
-the golden fixture generated by the unmodified reference and against the
-CPU restatement (oracle/) on seeded batches.  Bit-exact: verdicts, every
-rule's value (hits << 6 | flags) and the per-action stats.
+the regression fixture (tests/golden/, restatement-derived: make_golden.py
+runs oracle/xf_oracle.c; it pins regressions, the reference-held
+expectations are tests/kat.py's rows, checked by test_kat_counters.py) and
+against the CPU restatement (oracle/) on seeded batches.  Bit-exact:
+verdicts, every rule's value (hits << 6 | flags) and the per-action stats.
 """
 import errno
 
@@ -49,7 +51,7 @@ def assert_same(a_verd, a_rules, a_stats, b_verd, b_rules, b_stats):
 
 @pytest.mark.parametrize("tag", ["kat", "fuzz"])
 @pytest.mark.parametrize("variant", VARIANTS)
-def test_golden_on_gpu(G, golden, tag, variant):
+def test_restatement_fixture_on_gpu(G, golden, tag, variant):
     g = golden
     rules = golden_rules(g, f"{tag}_rules_")
     data, lens, stride = g[f"{tag}_data"], g[f"{tag}_lens"], int(g["stride"])

@@ -54,6 +54,7 @@ def _check(G, rules, data, lens):
     f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=1_000_000)
     f.load_rules(rules)
     v = f.run(data, lens, stride=64)
+    assert f.last_path() == f.PATH_QT   # the quotient index (1M dst rules)
     assert_same(v, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
     f.close()
     return ov, orules

@@ -30,7 +30,7 @@ def _check_against_golden(g, tag, variant, verdicts, after, stats):
 
 @pytest.mark.parametrize("tag", ["kat", "fuzz"])
 @pytest.mark.parametrize("variant", VARIANTS)
-def test_restatement_matches_golden(golden, tag, variant):
+def test_restatement_reproduces_own_regression_fixture(golden, tag, variant):
     g = golden
     rules = golden_rules(g, f"{tag}_rules_")
     data, lens, stride = g[f"{tag}_data"], g[f"{tag}_lens"], int(g["stride"])

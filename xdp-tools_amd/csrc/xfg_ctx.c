@@ -15,6 +15,7 @@
 #include "xdpfilter_gpu.h"
 
 #include <errno.h>
+#include <stddef.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -68,10 +69,18 @@ struct xfg_dev {
 	uint32_t port_tab_disp;
 	int port_tab_ok, port_tab_dirty;
 	/* resident classify workgroups per CU: [kernel: 0 general, 1 pipelined,
-	 * 2 pipelined IPv4-key mode, 3 split lookup pass, 4 split parse pass]
+	 * 2 pipelined IPv4-key mode, 3 split lookup pass, 4 split parse pass,
+	 * 5 pipelined IPv4-key mode over the quotient index]
 	 * [window 64, 128][dynamic LDS: none, direct counters, port nibble map,
 	 * both] */
-	int occ[5][2][4];
+	int occ[6][2][4];
+	/* quotient index of the IPv4 map (kind 5 kernel), uploaded from
+	 * ctx->qt when qt_gen falls behind ctx->qt_gen; params read at launch
+	 * under d->lock */
+	uint32_t *qt_img, *qt_trans;
+	uint64_t qt_img_bytes, qt_trans_bytes;
+	uint32_t qt_gen, qt_bits, qt_seed, qt_live, qt_n;
+	int last_kind;                  /* kernel kind of the last launch (-1: none) */
 	/* host-resident classify (xfg_classify_host / xfg_classify_xsk_host),
 	 * under host_lock: a gather pool, two fixed-size staging slots of
 	 * HOST_CH packets x HOST_WIN bytes (header windows, or whole slots of
@@ -117,7 +126,14 @@ struct xfg_ctx {
 	 * flag byte; flag_cnt[map][bit] = slots with that bit (likewise for the
 	 * ports).  The kernel skips a lookup whose mask no key carries. */
 	uint8_t *flag_or[NMAPS_HASH];
-	uint32_t flag_cnt[NMAPS_HASH][8];
+	uint32_t flag_cnt[NMAPS_HASH][8];   /* bit 7: slots whose flags differ between devices */
+	/* quotient index of the IPv4 map (xfg_table.h): rebuilt before a
+	 * classify that uses it when the map changed (qt_dirty); generation
+	 * qt_gen (0 = never built) */
+	struct xfg_qt qt;
+	int qt_dirty;
+	uint32_t qt_gen;
+	uint32_t qt_min_keys;
 	uint32_t port_flag_cnt[8];
 	/* multi-process reduction */
 	ncclComm_t comm;
@@ -128,6 +144,10 @@ struct xfg_ctx {
 	struct { const uint8_t *p; size_t bytes; } reg[XFG_HOST_REG_MAX];
 	int nreg;
 };
+
+/* Default smallest IPv4 map that takes the quotient index (its 2^17 buckets
+ * are 4 MiB: below this the canonical table and its prefilter stay in L2). */
+#define XFG_QT_MIN_KEYS (1u << 18)
 
 /* ------------------------------------------------------------------ misc */
 static const struct { const char *name; uint32_t feat; } prog_table[] = {
@@ -321,6 +341,8 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->red_stats);
 	hipFree(d->sink);
 	hipFree(d->port_tab);
+	hipFree(d->qt_img);
+	hipFree(d->qt_trans);
 	free(d->port_flags_h);
 	hipFree(d->cstatus);
 	for (int k = 0; k < 2; k++) {
@@ -404,9 +426,10 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 		goto fail;
 	}
 	d->port_tab_dirty = 1;
+	d->last_kind = -1;
 	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
-	for (int k = 0; k < 5; k++)
+	for (int k = 0; k < 6; k++)
 		for (int w = 0; w < 2; w++)
 			for (int c = 0; c < 4; c++)
 				d->occ[k][w][c] = xfg_classify_occupancy(
@@ -436,6 +459,9 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 		goto fail;
 
 	uint32_t seed = opts->hash_seed ? opts->hash_seed : 0x5eed1234u;
+	ctx->qt_min_keys = XFG_QT_MIN_KEYS;
+	if (opts->sz >= offsetof(struct xfg_open_opts, qt_min_keys) + sizeof(uint32_t) && opts->qt_min_keys)
+		ctx->qt_min_keys = opts->qt_min_keys;
 	uint32_t cap4 = opts->ipv4_capacity ? opts->ipv4_capacity : XFG_DEFAULT_MAP_CAPACITY;
 	uint32_t cap6 = opts->ipv6_capacity ? opts->ipv6_capacity : XFG_DEFAULT_MAP_CAPACITY;
 	uint32_t cape = opts->eth_capacity ? opts->eth_capacity : XFG_DEFAULT_MAP_CAPACITY;
@@ -515,6 +541,7 @@ void xfg_close(xfg_ctx *ctx)
 		free(ctx->host_vals[i]);
 		free(ctx->flag_or[i]);
 	}
+	xfg_qt_free(&ctx->qt);
 	free(ctx->host_port_vals);
 	free(ctx->port_flags_host);
 	pthread_mutex_destroy(&ctx->lock);
@@ -522,6 +549,13 @@ void xfg_close(xfg_ctx *ctx)
 }
 
 const char *xfg_prog_name(const xfg_ctx *ctx) { return ctx ? ctx->prog_name : NULL; }
+
+int xfg_last_path(const xfg_ctx *ctx, int dev)
+{
+	if (!ctx || dev < 0 || dev >= ctx->ndev)
+		return -EINVAL;
+	return ctx->dev[dev].last_kind < 0 ? -ENOENT : ctx->dev[dev].last_kind;
+}
 uint32_t xfg_prog_features(const xfg_ctx *ctx) { return ctx ? ctx->prog_features : 0; }
 int xfg_num_devices(const xfg_ctx *ctx) { return ctx ? ctx->ndev : -EINVAL; }
 
@@ -584,24 +618,31 @@ static void census(uint32_t *cnt, uint8_t old, uint8_t f)
 static uint32_t census_mask(const uint32_t *cnt)
 {
 	uint32_t m = 0;
-	for (int b = 0; b < 8; b++)
+	for (int b = 0; b < 6; b++)
 		if (cnt[b])
 			m |= 1u << b;
 	return m;
 }
 
-static void flags_note(xfg_ctx *ctx, int mi, uint64_t slot, uint8_t f)
+/* @any / @all: the OR / AND over devices of the slot's flag byte (bit 7 of
+ * the census byte records that they differ) */
+static void flags_note(xfg_ctx *ctx, int mi, uint64_t slot, uint8_t any, uint8_t all)
 {
+	const uint8_t f = any | (any != all ? 0x80 : 0);
 	census(ctx->flag_cnt[mi], ctx->flag_or[mi][slot], f);
 	ctx->flag_or[mi][slot] = f;
+	if (mi == 0)
+		ctx->qt_dirty = 1;
 }
 
 static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals)
 {
-	uint8_t any = 0;
-	for (int i = 0; i < (ctx->ndev ? ctx->ndev : 1); i++)
+	uint8_t any = 0, all = 63;
+	for (int i = 0; i < (ctx->ndev ? ctx->ndev : 1); i++) {
 		any |= vals[i] & 63;
-	flags_note(ctx, mi, slot, any);
+		all &= vals[i] & 63;
+	}
+	flags_note(ctx, mi, slot, any, all);
 	if (!ctx->ndev) {
 		ctx->host_vals[mi][slot] = vals[0];
 		return 0;
@@ -993,10 +1034,12 @@ static int update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t 
 			err = (int)s;
 			break;
 		}
-		uint8_t any = 0;
-		for (int d = 0; d < nv; d++)
+		uint8_t any = 0, all = 63;
+		for (int d = 0; d < nv; d++) {
 			any |= VAL(i, d) & 63;
-		flags_note(ctx, mi, (uint64_t)s, any);
+			all &= VAL(i, d) & 63;
+		}
+		flags_note(ctx, mi, (uint64_t)s, any, all);
 		if (nd) {
 			for (int d = 0; d < nd; d++) {
 				img[ib * d + xfg_table_flag_off(t, s)] = VAL(i, d) & 63;
@@ -1051,6 +1094,14 @@ int xfg_map_update_batch_percpu(xfg_ctx *ctx, int map, const void *keys, const u
  * (the only ones CHECK_MAP can test). */
 static int port_tab_refresh_locked(struct xfg_dev *d);
 
+
+/* Whether the count kernel's LDS histogram covers a QT of 2^bits buckets. */
+static int qt_hist_fits(uint32_t bits)
+{
+	const uint64_t span = (1ull << bits) * XFG_QT_SLOTS;
+	return ((span + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16 <= XFG_LOG_HIST_MAX;
+}
+
 static int port_tab_refresh(struct xfg_dev *d)
 {
 	/* (under the device lock: launch_batch reads the image's kind and
@@ -1094,6 +1145,41 @@ static int port_tab_refresh_locked(struct xfg_dev *d)
 		nib[k >> 3] |= (uint32_t)(d->port_flags_h[k] & 15) << ((k & 7) * 4);
 	int err = dev_write(d, d->port_nib, nib, XFG_PORT_NIB_WORDS * 4);
 	free(nib);
+	return err;
+}
+
+static int scratch(struct xfg_dev *d, void **p, uint64_t *have, uint64_t bytes);
+
+/* Bring the quotient index of the IPv4 map up to date for lookups of mask
+ * @live (ctx->lock held): rebuild the host image when the map changed, then
+ * upload it to @d when its copy is older (under d->lock: launch_batch reads
+ * the index's parameters there). */
+static int qt_refresh(xfg_ctx *ctx, struct xfg_dev *d, uint32_t live)
+{
+	int err = 0;
+	if (ctx->qt_dirty || !ctx->qt_gen || ctx->qt.live != live) {
+		if ((err = xfg_qt_build(&ctx->qt, &ctx->t[0], ctx->flag_or[0], live,
+					ctx->t[0].seed ^ 0x51ed2701u)))
+			return err;
+		ctx->qt_dirty = 0;
+		if (!++ctx->qt_gen)
+			ctx->qt_gen = 1;
+	}
+	if (d->qt_gen == ctx->qt_gen)
+		return 0;
+	const uint64_t ib = (1ull << ctx->qt.bits) * XFG_QT_BUCKET, tb = (uint64_t)ctx->qt.nslots * 4;
+	pthread_mutex_lock(&d->lock);
+	if (!(err = scratch(d, (void **)&d->qt_img, &d->qt_img_bytes, ib)) &&
+	    !(err = scratch(d, (void **)&d->qt_trans, &d->qt_trans_bytes, tb)) &&
+	    !(err = dev_write(d, d->qt_img, ctx->qt.img, ib)) &&
+	    !(err = dev_write(d, d->qt_trans, ctx->qt.trans, tb))) {
+		d->qt_gen = ctx->qt_gen;
+		d->qt_bits = ctx->qt.bits;
+		d->qt_seed = ctx->qt.seed;
+		d->qt_live = ctx->qt.live;
+		d->qt_n = ctx->qt.nslots;
+	}
+	pthread_mutex_unlock(&d->lock);
 	return err;
 }
 
@@ -1171,6 +1257,29 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 		a->port_count = 0;
 	}
 #endif
+	/* the quotient index (kind 5 kernel): the IPv4-key kernel with exactly
+	 * one live IPv4 lookup direction, the same flags on every device, and a
+	 * map large enough that the prefilter + bucket-line chain leaves L2;
+	 * its hit log must fit the count kernel's histogram */
+	if (a->pipe && a->km && !a->split) {
+		const int dl = a->t4.count && (a->t4.fmask & 2), sl = a->t4.count && (a->t4.fmask & 1);
+		const int ok = (dl ^ sl) && !ctx->flag_cnt[0][7] &&
+			       qt_hist_fits(xfg_qt_bits_for(a->t4.count));
+		int use = ok && a->t4.count >= ctx->qt_min_keys;
+#ifdef XFG_DIAG
+		const char *qo = getenv("XFG_QT");   /* "off" / "on" (any size) */
+		if (qo && !strcmp(qo, "off"))
+			use = 0;
+		else if (qo && !strcmp(qo, "on"))
+			use = ok;
+#endif
+		if (use) {
+			int err2 = qt_refresh(ctx, d, dl ? 2u : 1u);
+			if (err2)
+				return err2;
+			a->qt = d->qt_img;   /* (parameters: launch_batch, under d->lock) */
+		}
+	}
 	return 0;
 }
 
@@ -1202,11 +1311,13 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 {
 	int err = 0;
 	struct xfg_kargs a = *a0;
-	const int kind = a.pipe ? (a.km ? (a.split ? 3 : 2) : 1) : 0, wi = a.window > 64;
 	const char *cm = NULL;
 #ifdef XFG_DIAG
 	cm = getenv("XFG_COUNT");   /* diagnostics build only: "atomic" */
+	if (cm && !strcmp(cm, "atomic"))
+		a.qt = NULL;             /* (the QT kernel counts through the hit log only) */
 #endif
+	const int kind = a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
 	/* small rule sets: a direct LDS counter per hash-map slot (their few
 	 * counters are hot: more than the LDS counter cache holds) */
 	if (a.gbase[3] <= XFG_DCNT_MAX)
@@ -1219,6 +1330,14 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * d->lock for that): its kind and its longest displacement */
 	a.port_tab = d->port_tab_ok ? d->port_tab : NULL;
 	a.port_tab_disp = d->port_tab_disp;
+	if (a.qt) {   /* the index in stream order at this launch */
+		a.qt = d->qt_img;
+		a.qt_trans = d->qt_trans;
+		a.qt_bits = d->qt_bits;
+		a.qt_seed = d->qt_seed;
+		a.qt_live = d->qt_live;
+		a.qt_n = d->qt_n;
+	}
 	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
 #ifdef XFG_DIAG
 	const char *g = getenv("XFG_GRID_PER_CU");
@@ -1262,7 +1381,8 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * LDS counter, when the count kernel's histogram covers them; the wave
 	 * regions share the deferred lists' bound, the partition buffers hold
 	 * twice a uniform share (a fuller one spills to atomics) */
-	uint64_t total = (uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES;
+	/* (with the quotient index the log holds QT slots only: its span) */
+	uint64_t total = a.qt ? (uint64_t)a.qt_n : (uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES;
 	uint64_t hist = ((total + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
 	int logged = a.t4.count || a.t6.count || a.te.count;
 	if (a.pipe && logged && a.dcnt < a.gbase[3] && hist <= XFG_LOG_HIST_MAX &&
@@ -1283,6 +1403,10 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.pcap = (uint32_t)pcap;
 		a.log_hist = (uint32_t)hist;
 	}
+	if (a.qt && !a.tlog) {   /* (fill_kargs checked that the log covers the index) */
+		err = -EIO;
+		goto out;
+	}
 	if (user && user != (void *)d->stream) {
 		if ((err = hip_err(hipEventRecord(d->ev_user, (hipStream_t)user))) ||
 		    (err = hip_err(hipStreamWaitEvent(d->stream, d->ev_user, 0))))
@@ -1290,6 +1414,8 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	}
 	for (int i = 0; i < iters && !err; i++)
 		err = xfg_launch_classify(ctx->prog_features, &a, (unsigned)grid, d->stream);
+	if (!err)
+		d->last_kind = kind;
 	if (!err && user && user != (void *)d->stream) {
 		if (!(err = hip_err(hipEventRecord(d->ev_done, d->stream))))
 			err = hip_err(hipStreamWaitEvent((hipStream_t)user, d->ev_done, 0));

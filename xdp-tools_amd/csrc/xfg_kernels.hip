@@ -564,6 +564,13 @@ __device__ __forceinline__ unsigned long long *global_counter(const xfg_kargs &a
 	return a.t4.hits + g;
 }
 
+// Counter of hit-log entry g: a counter identity, or with the quotient index
+// (kargs.qt) a QT slot, whose canonical identity qt_trans holds.
+__device__ __forceinline__ unsigned long long *log_counter(const xfg_kargs &a, uint32_t g)
+{
+	return global_counter(a, a.qt ? a.qt_trans[g] : g);
+}
+
 // CHECK_MAP (xdp-filter/xdpfilt_prog.h:56-64): hit iff the key exists and
 // (value & mask) == mask; the counter bump is deferred to the caller.
 __device__ __forceinline__ bool take(const Hit &h, uint32_t mask, uint32_t base, uint32_t &tag)
@@ -993,7 +1000,7 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 			if (pos < a.pcap)
 				gst32(a.pbuf + (uint64_t)p * a.pcap + pos, x);
 			else
-				atomicAdd(global_counter(a, x), 1ull);
+				atomicAdd(log_counter(a, x), 1ull);
 		}
 		__syncthreads();
 		for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
@@ -1207,6 +1214,7 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 }
 
 #include "xfg_pipeline.hip"
+#include "xfg_pipeq.hip"
 #ifdef XFG_DIAG   // measured slower than xfg_pipe4_kernel: diagnostics only
 #include "xfg_split.hip"
 #endif
@@ -1244,11 +1252,12 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	__syncthreads();
 	if (tid == 0)
 		a.pfill[p] = 0;
-	const uint32_t total = a.gbase[3] + 65536u;   // + the port counters
+	// the identity span: hash-map + port counters, or the QT slots
+	const uint32_t total = a.qt ? a.qt_n : a.gbase[3] + 65536u;
 	for (uint32_t k = tid; k < hist_n; k += LC_THREADS) {
 		const uint32_t g = ((k >> 4) << 12) | (p << 4) | (k & 15);
 		if (hist[k] && g < total)
-			*global_counter(a, g) += hist[k];
+			*log_counter(a, g) += hist[k];
 	}
 }
 
@@ -1280,7 +1289,18 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 					hipLaunchKernelGGL((xfg_look4_kernel<FEAT, 128>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
 			} else
 #endif
-			if (a.km == 1) {
+			if (a.km == 1 && a.qt) {
+				// the quotient index: one bucket read per packet
+				done = true;
+				if (a.window <= 64 && a.dense)
+					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
+				else if (a.window <= 64)
+					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
+				else if (a.dense)
+					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
+				else
+					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
+			} else if (a.km == 1) {
 				done = true;
 				if (a.window <= 64 && a.dense)
 					hipLaunchKernelGGL((xfg_pipe4_kernel<FEAT, 64, true>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
@@ -1345,7 +1365,8 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 
 // Resident workgroups per CU of a classify kernel (persistent grid sizing)
 // with `dyn` bytes of dynamic LDS: kind 0 = general, 1 = pipelined (key
-// mode 0), 2 = pipelined (key mode 1); window 64 or 128.
+// mode 0), 2 = pipelined (key mode 1), 5 = pipelined over the quotient
+// index; window 64 or 128.
 template <uint32_t FEAT>
 static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 {
@@ -1371,6 +1392,11 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 			e = window <= 64
 				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 64, true>, PIPE_THREADS(64), dyn)
 				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 128, false>, PIPE_THREADS(128), dyn);
+		} else if (kind == 5) {
+			done = true;
+			e = window <= 64
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true>, PIPE_THREADS(64), dyn)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false>, PIPE_THREADS(128), dyn);
 		}
 	}
 	if (done)

@@ -39,6 +39,18 @@
  * (false positives only; the bucket probe decides), and the host rebuilds
  * the filter when stale bits accumulate.
  *
+ * Quotient index ("QT", xfg_table.h xfg_qt): a derived, read-only index of
+ * the IPv4 map that answers a lookup with ONE random 32-byte read and no
+ * prefilter, for the pipelined IPv4-key kernel when exactly one lookup
+ * direction can hit.  h = xfg_qt_hash(key) is a bijection of the 32-bit key,
+ * so (bucket = h >> (32 - bits), remainder = h's low 32 - bits <= 15 bits)
+ * identifies the key exactly.  A bucket is 16 u16: entry 0 = count (bits
+ * 0-3) | overflow (bit 15: a key homed here did not fit; a miss here is
+ * decided by the canonical table instead), entries 1..count = remainder |
+ * live << 15 (live: the key's flags carry the one live mask).  QT slot
+ * bucket * 15 + entry - 1 maps back to the canonical slot through
+ * trans[] (the count kernel's job).
+ *
  * filter_ports (PERCPU_ARRAY[65536], :67-73) is dense: flags[65536] u8 and
  * hits[65536] u64 indexed by the raw big-endian port value, plus a 65536-bit
  * "any flag set" bitmap that each workgroup stages in LDS.
@@ -63,6 +75,11 @@
 #define XFG_PORT_NIB_WORDS 8192u  /* more: every port's 4 flag bits, 32 KiB of LDS */
 
 #define XFG_BLOOM_K       4u
+
+#define XFG_QT_SLOTS      15u     /* entries per 32-byte QT bucket */
+#define XFG_QT_BUCKET     32u
+#define XFG_QT_MIN_BITS   17u     /* remainders of at most 15 bits */
+#define XFG_QT_OVF        0x8000u
 
 #define XFG_DCNT_MAX      4096u   /* direct LDS counters (16 KiB) */
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
@@ -155,6 +172,16 @@ struct xfg_kargs {
 	uint32_t grid_parse;
 	uint32_t bloom_off;
 	uint32_t *rec_ka, *rec_kb, *rec_port;
+	/* Quotient index of the IPv4 map (NULL = none): 1 << qt_bits buckets;
+	 * its slots are counter identities qt_base + slot (after the ports),
+	 * mapped to canonical ones by qt_trans; qt_live = the one live mask */
+	const uint32_t *qt;
+	const uint32_t *qt_trans;
+	uint32_t qt_bits;
+	uint32_t qt_seed;
+	uint32_t qt_base;
+	uint32_t qt_n;
+	uint32_t qt_live;
 };
 
 
@@ -211,6 +238,13 @@ XFG_HD uint32_t xfg_bloom_mask(uint32_t h)
 	uint32_t g = xfg_fmix32(h ^ 0x7f4a7c15u);
 	return (1u << (g & 31)) | (1u << ((g >> 5) & 31)) | (1u << ((g >> 10) & 31)) |
 	       (1u << ((g >> 15) & 31));
+}
+
+/* The QT index's key hash: a bijection of the 32-bit key (xor with the
+ * seed, then the murmur3 finaliser: each step is invertible). */
+XFG_HD uint32_t xfg_qt_hash(uint32_t k, uint32_t seed)
+{
+	return xfg_fmix32(k ^ seed);
 }
 
 /* Home slot of a port key in the LDS port table. */

@@ -238,3 +238,64 @@ void xfg_table_desc(const struct xfg_table *t, struct xfg_tdesc *d)
 	d->seed = t->seed;
 	d->bloom_words = t->bloom_words;
 }
+
+/* ------------------------------------------------------------ quotient index */
+uint32_t xfg_qt_bits_for(uint32_t count)
+{
+	uint32_t b = XFG_QT_MIN_BITS;
+	while (b < 30 && ((uint64_t)count >> b) > 8)
+		b++;
+	return b;
+}
+
+void xfg_qt_free(struct xfg_qt *q)
+{
+	free(q->img);
+	free(q->trans);
+	q->img = NULL;
+	q->trans = NULL;
+}
+
+int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *flags,
+		 uint32_t live, uint32_t seed)
+{
+	if (t->keylen != 4)
+		return -EINVAL;
+	const uint32_t bits = xfg_qt_bits_for(t->count);
+	const uint64_t nb = 1ull << bits, ns = nb * XFG_QT_SLOTS;
+	if (q->bits != bits || !q->img) {
+		xfg_qt_free(q);
+		q->img = malloc(nb * XFG_QT_BUCKET);
+		q->trans = malloc(ns * 4);
+		if (!q->img || !q->trans) {
+			xfg_qt_free(q);
+			return -ENOMEM;
+		}
+	}
+	memset(q->img, 0, nb * XFG_QT_BUCKET);
+	memset(q->trans, 0xff, ns * 4);
+	q->bits = bits;
+	q->seed = seed;
+	q->live = live;
+	q->nslots = (uint32_t)ns;
+	q->placed = q->spilled = 0;
+	const uint32_t rbits = 32 - bits, rmask = (1u << rbits) - 1;
+	for (int64_t s = xfg_table_next_slot(t, -1); s >= 0; s = xfg_table_next_slot(t, s)) {
+		uint32_t k;
+		xfg_table_slot_key(t, (uint64_t)s, &k);   /* the wire bytes, as the kernel loads them */
+		const uint32_t h = xfg_qt_hash(k, seed), b = h >> rbits;
+		uint16_t *e = q->img + (uint64_t)b * 16;
+		const uint32_t c = e[0] & 15;
+		if (c == XFG_QT_SLOTS) {   /* full: the canonical table answers this bucket's misses */
+			e[0] |= XFG_QT_OVF;
+			q->spilled++;
+			continue;
+		}
+		const uint32_t lv = (flags[s] & live) == live;
+		e[1 + c] = (uint16_t)((h & rmask) | (lv << 15));
+		e[0] = (uint16_t)((e[0] & XFG_QT_OVF) | (c + 1));
+		q->trans[(uint64_t)b * XFG_QT_SLOTS + c] = (uint32_t)s;
+		q->placed++;
+	}
+	return 0;
+}

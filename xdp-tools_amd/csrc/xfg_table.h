@@ -76,6 +76,23 @@ static inline uint64_t xfg_table_img_bytes(const struct xfg_table *t)
 	return ((uint64_t)t->nbuckets + 1) * XFG_BUCKET_BYTES;
 }
 
+/* Quotient index of a table of 4-byte keys (layout: xfg_layout.h).  Built
+ * from the table's keys and each slot's flag byte (@flags[slot], the same on
+ * every device); entries answer lookups of mask @live.  Returns 0 or
+ * -ENOMEM / -EINVAL (not 4-byte keys). */
+struct xfg_qt {
+	uint32_t bits, seed, live;
+	uint32_t nslots;      /* (1 << bits) * XFG_QT_SLOTS */
+	uint16_t *img;        /* (1 << bits) * 16 entries */
+	uint32_t *trans;      /* nslots: canonical slot, or ~0u */
+	uint32_t placed, spilled;
+};
+int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *flags,
+		 uint32_t live, uint32_t seed);
+void xfg_qt_free(struct xfg_qt *q);
+/* Bucket bits for @count keys: at most ~8 keys per 15-entry bucket. */
+uint32_t xfg_qt_bits_for(uint32_t count);
+
 /* Descriptor for the kernel (device pointers filled by the caller). */
 void xfg_table_desc(const struct xfg_table *t, struct xfg_tdesc *d);
 

@@ -52,7 +52,7 @@ EXPORTS = [
     "xfg_host_alloc_pinned", "xfg_host_free_pinned", "xfg_classify_timed", "xfg_stream_read_timed",
     "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce", "xfg_map_update_batch_percpu",
     "xfg_classify_descs", "xfg_compact", "xfg_classify_xsk_host", "xfg_host_register",
-    "xfg_host_unregister",
+    "xfg_host_unregister", "xfg_last_path",
 ]
 # include/xdpfilter_io.h
 IO_EXPORTS = [
@@ -67,7 +67,8 @@ class OpenOpts(C.Structure):
     _fields_ = [("sz", C.c_size_t), ("features", C.c_uint32),
                 ("devices", C.POINTER(C.c_int)), ("ndev", C.c_int),
                 ("ipv4_capacity", C.c_uint32), ("ipv6_capacity", C.c_uint32),
-                ("eth_capacity", C.c_uint32), ("hash_seed", C.c_uint32)]
+                ("eth_capacity", C.c_uint32), ("hash_seed", C.c_uint32),
+                ("qt_min_keys", C.c_uint32)]
 
 
 class Batch(C.Structure):
@@ -104,6 +105,7 @@ def _load():
         "xfg_prog_features": (C.c_uint32, [vp]),
         "xfg_num_devices": (C.c_int, [vp]),
         "xfg_strerror": (C.c_char_p, [C.c_int]),
+        "xfg_last_path": (C.c_int, [vp, C.c_int]),
         "xfg_map_lookup": (C.c_int, [vp, C.c_int, vp, u64p]),
         "xfg_map_update": (C.c_int, [vp, C.c_int, vp, u64p]),
         "xfg_map_delete": (C.c_int, [vp, C.c_int, vp]),
@@ -260,7 +262,7 @@ class Filter:
     """One xfg context: a selected xdpfilt_* program, its maps, and devices."""
 
     def __init__(self, features=FEAT_ALL | FEAT_DENY, devices=None, ndev=None,
-                 ipv4_capacity=0, ipv6_capacity=0, eth_capacity=0, hash_seed=0):
+                 ipv4_capacity=0, ipv6_capacity=0, eth_capacity=0, hash_seed=0, qt_min_keys=0):
         opts = OpenOpts()
         opts.sz = C.sizeof(OpenOpts)
         opts.features = features
@@ -275,6 +277,7 @@ class Filter:
         opts.ipv6_capacity = ipv6_capacity
         opts.eth_capacity = eth_capacity
         opts.hash_seed = hash_seed
+        opts.qt_min_keys = qt_min_keys
         ctx = C.c_void_p()
         _check(lib.xfg_open(C.byref(ctx), C.byref(opts)), "xfg_open")
         self.ctx = ctx
@@ -492,6 +495,12 @@ class Filter:
 
     def stats_reset(self):
         _check(lib.xfg_stats_reset(self.ctx), "stats_reset")
+
+    PATH_GENERAL, PATH_PIPELINE, PATH_IPV4, PATH_QT = 0, 1, 2, 5
+
+    def last_path(self, dev=0) -> int:
+        """The classify kernel of the last launch on @dev (xfg_last_path)."""
+        return _check(lib.xfg_last_path(self.ctx, dev), "last_path")
 
     def sync(self):
         _check(lib.xfg_sync(self.ctx), "sync")
