@@ -312,6 +312,11 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 	if (k < iters)
 		iteration(k, preA, lenA);
 
+#ifdef XFG_DIAG
+	// (diagnostics: 2048 skips the deferred packets -- results wrong)
+	if (a.diag & 2048)
+		ndef = 0;
+#endif
 	// the deferred packets: the whole reference walk over the canonical
 	// table (classify_staged), 64 at a time
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
@@ -350,6 +355,10 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 			for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
 				if (s_pcnt[i])
 					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
+#ifdef XFG_DIAG
+	if (a.diag & 16)   // (diagnostics: no workgroup-end partition -- counts wrong)
+		return;
+#endif
 	if (a.tlog)   // (win is free now: the partition scratch)
 		log_partition<NW>(a, s_tn, s_lh, win, tid);
 }
