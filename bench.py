@@ -36,6 +36,37 @@ HBM_PEAK_GBS = 8000.0
 REDUCE_TIMEOUT_S = 120.0   # the readout all-reduce (outside the timed region)
 
 
+# the classify kernel each launch path runs (xfg_last_path)
+KERNEL_OF_PATH = {
+    0: "xfg_classify_kernel (general)",
+    1: "xfg_pipeline_kernel (generic pipelined)",
+    2: "xfg_pipe4_kernel (IPv4-key pipelined)",
+    5: "xfg_pipeq_kernel (IPv4-key pipelined over the quotient index)",
+}
+# rocprofv3 --pmc summaries of the bench's own workload (tools/pmc.sh,
+# tools/pmc_summary.py): per launch path, the file and the batch it was taken at
+PMC_OF_PATH = {5: ("profiles/r03_c3_pmc_2p26.json", 1 << 26)}
+
+
+def committed_traffic(path, n, stream_bytes):
+    """HBM bytes per launch from the committed PMC passes of this path's
+    kernel at this batch, or None when no such file matches.  gfx950's
+    FETCH_SIZE tallies a wide coalesced read at half its bytes and a random
+    32/64-byte line at its bytes (profiles/r02_fetch_size_calibration.json),
+    so the frame + length stream's other half is added back, not the whole
+    figure doubled; WRITE_SIZE as read."""
+    ent = PMC_OF_PATH.get(path)
+    if not ent or ent[1] != n or not os.path.exists(os.path.join(ROOT, ent[0])):
+        return None, "null: no committed PMC pass of this kernel at this batch"
+    d = json.load(open(os.path.join(ROOT, ent[0])))
+    if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+        return None, f"null: {ent[0]} lacks FETCH_SIZE/WRITE_SIZE"
+    t = int(d["FETCH_SIZE"] * 1024 + stream_bytes / 2 + d["WRITE_SIZE"] * 1024)
+    return t, (f"{ent[0]} (separate rocprofv3 --pmc runs of the same kernel and workload): "
+               "FETCH_SIZE + half the frame/length stream (tallied at half on gfx950) "
+               "+ WRITE_SIZE, per launch")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -222,10 +253,12 @@ def main():
         cpu = cpu_baseline(X, np, v4, ports, args.cpu_seconds)
 
     # ---- traffic: PMC bytes cannot be counted inside this timed process
-    # (a rocprofv3 --pmc pass is its own run); the per-launch FETCH/WRITE
-    # figures of this kernel are committed under profiles/ 
-    traffic = None
-    traffic_src = "null here: rocprofv3 --pmc passes of this kernel in profiles/r02_c3_pmc.json"
+    # (a rocprofv3 --pmc pass is its own run): the per-launch figures of the
+    # same kernel on the same workload, committed under profiles/ (DESIGN.md
+    # §6), corrected as MI355X_MICROARCH.md's HBM section prescribes
+    path = f.last_path()
+    kname = KERNEL_OF_PATH.get(path, f"path {path}")
+    traffic, traffic_src = committed_traffic(path, n, n * stride + n * 2)
 
     total_pkts = n * args.steps * world
     value = total_pkts / wall / 1e6
@@ -261,8 +294,8 @@ def main():
             "traffic": traffic,
             "alg_bytes_per_launch": alg_bytes,
             "kernel_ms": round(kern_ms, 4),
-            "kernel": "one classify pass: xfg_pipe4_kernel (IPv4-key pipelined classify) + "
-                      "xfg_log_count_kernel (hit-log counts), HIP events on the launch stream",
+            "kernel": f"one classify pass: {kname} + xfg_log_count_kernel (hit-log counts), "
+                      "HIP events on the launch stream",
             "peak_measured_stream_read": round(peak_meas, 1),
             "frac_of_measured": round(achieved / peak_meas, 4),
             "traffic_source": traffic_src,

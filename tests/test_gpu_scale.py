@@ -1,15 +1,16 @@
 """GPU parity at the bench's own batch size (SURVEY.md §8d's C3, as bench.py
-runs it): everything sized by the batch -- the hit-log partition buffers
-(2 n / 256 + 1024 entries each, spilling to atomics past that,
-xfg_ctx.c launch_batch), the per-wave deferred lists and hit-log regions,
+runs it): everything sized by the batch -- the hit-log partition
+sub-buffers (2 n / 2048 + 256 entries each, 8 per partition, spilling to
+atomics past that, xfg_ctx.c launch_batch), the per-wave deferred lists and hit-log regions,
 the count kernel -- is checked against the CPU restatement (oracle/) on
 every host thread, bit-exact: verdicts, all 1M rule values, per-action
 stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
 
   * C3 at 2^26 packets, 16-bit lengths: bench.py's rank-0 shard exactly;
   * a skewed C3 at 2^25: every hit on one of 8 hot rules, so each hot
-    rule's hits alone (~1.9M) overfill its hit-log partition (~263k
-    entries): the spill-to-atomics path runs at scale.
+    rule's hits alone (~1.9M) overfill its hit-log partition's
+    sub-buffers (8 x ~33k entries): the spill-to-atomics path runs at
+    scale.
 """
 import os
 
@@ -79,7 +80,8 @@ def test_c3_skewed_hits_overfill_log_partitions_2p25(G):
     data, lens = X.gen_workload(33, 3, n, 64, v4=hot, ports=ports, dst_permille=500,
                                 port_permille=250, bad_permille=10)
     _, orules = _check(G, rules, data, lens.astype(np.uint16))
-    pcap = 2 * ((n + 255) // 256) + 1024
+    pcap = 8 * (2 * ((n + 2047) // 2048) + 256)   # a partition's 8 sub-buffers
     hits = orules.v4_vals[:8] >> 6
     assert (hits > pcap).all(), (hits, pcap)   # each hot rule alone overfills a partition
-    assert int((orules.v4_vals[8:] >> 6).sum()) == 0
+    # (the other rules only see random addresses that happen to be ruled)
+    assert int((orules.v4_vals[8:] >> 6).sum()) < n // 1000

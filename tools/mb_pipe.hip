@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64 * NWV) void k_skel(const Args a)
 			// ---- Q(k-1): its Bloom word -> bucket; line LDS-DMA'd into
 			// buffer (k-1)&1 (read by R in the next iteration)
 			const uint32_t q_w = bwb[((k + 1) & 1) * 64 + lane];
-			sel = vQ && ((q_h ^ q_w) & 1);
+			sel = vQ && (((q_h ^ q_w) & 1) || (a.flags & 16));
 			q_fb = q_w & 1;
 			const uint32_t bk = __umulhi(q_h, a.nb);
 			const uint32_t lbuf = lds_addr(lin + ((k + 1) & 1) * 1024);
@@ -383,6 +383,11 @@ int main(int argc, char **argv)
 	struct Case { const char *name; uint32_t flags, bw, nb; };
 	const Case cases[] = {
 		{ "stream+store", 4, bw, nb },
+		{ "stream+1line/pkt 2MB+store", 22, bw, 32768 },
+		{ "stream+1line/pkt 2.8MB+store", 22, bw, 45875 },
+		{ "stream+1line/pkt 4MB+store", 22, bw, 65536 },
+		{ "stream+1line/pkt 5.3MB+store", 22, bw, 86800 },
+		{ "stream+1line/pkt 9MB+store", 22, bw, nb },
 		{ "stream+bloom1.5MB+store", 5, bw, nb },
 		{ "stream+lines9MB+store", 6, bw, nb },
 		{ "stream+lines2MB+store", 6, bw, 32768 },
@@ -395,6 +400,8 @@ int main(int argc, char **argv)
 		{ "nostream+lines16KB", 10, bw, 256 },
 	};
 	for (const Case &c : cases) {
+		if (!(c.flags & 16) && c.flags != 4 && c.flags != 7)
+			continue;
 		Args b = a;
 		b.flags = c.flags;
 		b.bw = c.bw;

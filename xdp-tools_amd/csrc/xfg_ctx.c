@@ -100,8 +100,9 @@ struct xfg_dev {
 	int lock_ok;
 	uint32_t *defer;                /* pipelined kernel: deferred-packet lists */
 	uint64_t defer_bytes;
-	uint32_t *tlog, *pbuf, *pfill;  /* hit log: wave regions, partition buffers, fills */
-	uint64_t tlog_bytes, pbuf_bytes;
+	uint32_t *tlog, *pfill;         /* hit log: wave regions, slice fills */
+	uint16_t *pbuf;                 /* hit log: partition slices */
+	uint64_t tlog_bytes, pbuf_bytes, pfill_bytes;
 	uint32_t *rec;                  /* split classify: parse-pass records */
 	uint64_t rec_bytes;
 	unsigned long long *cstatus;    /* verdict compaction: tile status words */
@@ -1386,21 +1387,24 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	uint64_t hist = ((total + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
 	int logged = a.t4.count || a.t6.count || a.te.count;
 	if (a.pipe && logged && a.dcnt < a.gbase[3] && hist <= XFG_LOG_HIST_MAX &&
+	    grid <= XFG_LOG_SLICES_MAX &&
 	    !(cm && !strcmp(cm, "atomic"))) {
-		uint64_t pcap = 2 * ((a.n + XFG_LOG_PARTS - 1) / XFG_LOG_PARTS) + 1024;
+		/* slice (partition, workgroup): twice a uniform share of the
+		 * most the workgroup's waves can log (a fuller one spills) */
+		uint64_t wg_max = (per_wg / 64) * (uint64_t)a.defer_cap;
+		uint64_t pcap = (2 * ((wg_max + XFG_LOG_PARTS - 1) / XFG_LOG_PARTS) + 64 + 7) & ~7ull;
 		if ((err = scratch(d, (void **)&d->tlog, &d->tlog_bytes,
 				   grid * (per_wg / 64) * (uint64_t)a.defer_cap * 4)) ||
-		    (err = scratch(d, (void **)&d->pbuf, &d->pbuf_bytes, XFG_LOG_PARTS * pcap * 4)))
+		    (err = scratch(d, (void **)&d->pbuf, &d->pbuf_bytes,
+				   ((uint64_t)XFG_LOG_PARTS * grid * pcap + 512) * 2)) ||   /* (+ the count kernel's overread) */
+		    (err = scratch(d, (void **)&d->pfill, &d->pfill_bytes,
+				   (uint64_t)XFG_LOG_PARTS * grid * 4)))
 			goto out;
-		if (!d->pfill) {
-			if ((err = hip_err(hipMalloc((void **)&d->pfill, XFG_LOG_PARTS * 4))) ||
-			    (err = hip_err(hipMemsetAsync(d->pfill, 0, XFG_LOG_PARTS * 4, d->stream))))
-				goto out;
-		}
 		a.tlog = d->tlog;
 		a.pbuf = d->pbuf;
 		a.pfill = d->pfill;
 		a.pcap = (uint32_t)pcap;
+		a.pslices = (uint32_t)grid;
 		a.log_hist = (uint32_t)hist;
 	}
 	if (a.qt && !a.tlog) {   /* (fill_kargs checked that the log covers the index) */

@@ -892,6 +892,23 @@ __device__ __forceinline__ void log_append(uint32_t *region, uint32_t &cnt, uint
 #ifndef XFG_LOG_CHUNK
 #define XFG_LOG_CHUNK 8192
 #endif
+#ifndef XFG_PART_LDSBAR
+#define XFG_PART_LDSBAR 1
+#endif
+
+// A workgroup barrier for LDS hand-offs only: the waves' LDS operations are
+// complete (lgkmcnt(0)) but their global loads and stores stay in flight
+// (__syncthreads() also drains vmcnt, which would serialise the partition's
+// chunk prefetch and write-out on every barrier).  The memory clobber keeps
+// the compiler from moving memory accesses across it.
+__device__ __forceinline__ void lds_barrier()
+{
+#if XFG_PART_LDSBAR
+	asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+	__syncthreads();
+#endif
+}
 constexpr uint32_t LOG_CHUNK = XFG_LOG_CHUNK;
 constexpr uint32_t LOG_SCRATCH = 4 * XFG_LOG_PARTS + LOG_CHUNK;   // words
 
@@ -903,11 +920,14 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 	static_assert(LOG_CHUNK % NTH == 0, "chunk: whole entries per thread");
 	const int nthr = NTH;
 	uint32_t *const s_h = s;                         // histogram, then the chunk's counts
-	uint32_t *const s_b = s + XFG_LOG_PARTS;         // the workgroup's slice of each buffer
 	uint32_t *const s_cur = s + 2 * XFG_LOG_PARTS;   // entries written per partition
 	uint32_t *const s_off = s + 3 * XFG_LOG_PARTS;   // the chunk's run starts
 	uint32_t *const s_srt = s + 4 * XFG_LOG_PARTS;   // the chunk, sorted
 	const uint64_t r0 = (uint64_t)blockIdx.x * NW * a.defer_cap;
+	// this workgroup's slice of every partition: position 0, its count
+	// stored for the count kernel (entries past pcap spill to atomics)
+	const uint64_t slice0 = (uint64_t)blockIdx.x * a.pcap;
+	const uint64_t pstep = (uint64_t)a.pslices * a.pcap;
 	for (int i = tid; i < (int)XFG_LOG_PARTS; i += nthr) {
 		s_h[i] = 0;
 		s_cur[i] = 0;
@@ -922,11 +942,14 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 	}
 	__syncthreads();
 	for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
-		const uint32_t c = s_hist ? s_hist[p] : s_h[p];
-		s_b[p] = c ? atomicAdd(&a.pfill[p], c) : 0;
+		gst32(a.pfill + (uint64_t)p * a.pslices + blockIdx.x, s_hist ? s_hist[p] : s_h[p]);
 		s_h[p] = 0;
 	}
 	__syncthreads();
+#ifdef XFG_DIAG
+	if (a.diag & 1024)   // diagnostics: stop after the reservations (counts wrong)
+		return;
+#endif
 	// the NW regions as one sequence (entry e of region w at pre[w] + e),
 	// cut into chunks of LOG_CHUNK: runs of about LOG_CHUNK / 256 entries
 	uint32_t pre[NW + 1];
@@ -961,7 +984,7 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 #pragma unroll
 		for (int j = 0; j < K; j++)
 			rk[j] = g[j] != CT_NONE ? atomicAdd(&s_h[log_part(g[j])], 1u) : 0u;
-		__syncthreads();
+		lds_barrier();
 		// run starts: exclusive scan of the counts (one wave)
 		if (tid < 64) {
 			uint32_t v[XFG_LOG_PARTS / 64], sum = 0;
@@ -984,30 +1007,31 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 				run += v[q];
 			}
 		}
-		__syncthreads();
+		lds_barrier();
 #pragma unroll
 		for (int j = 0; j < K; j++)
 			if (g[j] != CT_NONE)
 				s_srt[s_off[log_part(g[j])] + rk[j]] = g[j];
 		if (c0 + LOG_CHUNK < total)
 			fetch(c0 + LOG_CHUNK);
-		__syncthreads();
+		lds_barrier();
 		for (uint32_t t = tid; t < cn; t += nthr) {
 			const uint32_t x = s_srt[t], p = log_part(x);
-			const uint32_t pos = s_b[p] + s_cur[p] + (t - s_off[p]);
+			const uint32_t pos = s_cur[p] + (t - s_off[p]);
 			if (a.diag & 256)   // diagnostics build only: no write-out
 				continue;
-			if (pos < a.pcap)
-				gst32(a.pbuf + (uint64_t)p * a.pcap + pos, x);
+			if (pos < a.pcap)   // (the partition is implied: the local index)
+				*reinterpret_cast<__attribute__((address_space(1))) uint16_t *>(
+					(uintptr_t)(a.pbuf + p * pstep + slice0 + pos)) = (uint16_t)log_local(x);
 			else
 				atomicAdd(log_counter(a, x), 1ull);
 		}
-		__syncthreads();
+		lds_barrier();
 		for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
 			s_cur[p] += s_h[p];
 			s_h[p] = 0;
 		}
-		__syncthreads();
+		lds_barrier();
 	}
 }
 
@@ -1220,44 +1244,84 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 #endif
 
 // ---------------------------------------------------------------- hit-log count
-// One workgroup per log partition (see HitLog): sums the partition's buffer
-// in an LDS histogram, then adds each non-zero count to its counter with a
-// plain read-modify-write (the workgroup owns the partition's counters),
-// and resets the partition's fill for the next launch.
+// One workgroup per log partition (see HitLog): sums the partition's
+// slices (one per classify workgroup, 16-bit local indices) in an LDS
+// histogram, then adds each non-zero count to its counter with a plain
+// read-modify-write (the workgroup owns the partition's counters).  The
+// counters' current values (and, for the quotient index, their identities)
+// are read before the histogram is built, so the end is one round of
+// stores.  A wave per slice, eight slices in flight per wave, one 8-byte
+// load per lane (a wave load covers 256 entries: about a uniform slice, so
+// few of the LDS atomics' lanes idle).
 constexpr int LC_THREADS = 1024;
 
 __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kargs a, uint32_t hist_n)
 {
 	extern __shared__ uint32_t hist[];
-	const uint32_t tid = threadIdx.x, p = blockIdx.x;
-	const uint32_t fill = a.pfill[p];
-	const uint32_t np = fill < a.pcap ? fill : a.pcap;
-	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
-		hist[i] = 0;
-	__syncthreads();
-	const uint32_t *e = a.pbuf + (uint64_t)p * a.pcap;
-	uint32_t i = tid;
-	for (; i + 3 * LC_THREADS < np; i += 4 * LC_THREADS) {
-		const uint32_t g0 = __builtin_nontemporal_load(e + i);
-		const uint32_t g1 = __builtin_nontemporal_load(e + i + LC_THREADS);
-		const uint32_t g2 = __builtin_nontemporal_load(e + i + 2 * LC_THREADS);
-		const uint32_t g3 = __builtin_nontemporal_load(e + i + 3 * LC_THREADS);
-		atomicAdd(&hist[log_local(g0)], 1u);
-		atomicAdd(&hist[log_local(g1)], 1u);
-		atomicAdd(&hist[log_local(g2)], 1u);
-		atomicAdd(&hist[log_local(g3)], 1u);
-	}
-	for (; i < np; i += LC_THREADS)
-		atomicAdd(&hist[log_local(__builtin_nontemporal_load(e + i))], 1u);
-	__syncthreads();
-	if (tid == 0)
-		a.pfill[p] = 0;
+	__shared__ uint32_t s_fill[XFG_LOG_SLICES_MAX];
+	const uint32_t tid = threadIdx.x, p = blockIdx.x, lane = tid & 63, w = tid >> 6;
+	constexpr uint32_t NWV = LC_THREADS / 64, U = 8, J = XFG_LOG_HIST_MAX / LC_THREADS;
+	const uint32_t S = a.pslices, cap = a.pcap;
 	// the identity span: hash-map + port counters, or the QT slots
 	const uint32_t total = a.qt ? a.qt_n : a.gbase[3] + 65536u;
-	for (uint32_t k = tid; k < hist_n; k += LC_THREADS) {
+	// counters of histogram entries tid + j * LC_THREADS: identity, value
+	uint32_t gid[J];
+	unsigned long long val[J];
+#pragma unroll
+	for (uint32_t j = 0; j < J; j++) {
+		const uint32_t k = tid + j * LC_THREADS;
 		const uint32_t g = ((k >> 4) << 12) | (p << 4) | (k & 15);
-		if (hist[k] && g < total)
-			*log_counter(a, g) += hist[k];
+		gid[j] = k < hist_n && g < total ? (a.qt ? a.qt_trans[g] : g) : CT_NONE;
+	}
+	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * S + tid] : 0u;
+	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
+		hist[i] = 0;
+#pragma unroll
+	for (uint32_t j = 0; j < J; j++)
+		val[j] = gid[j] != CT_NONE ? *global_counter(a, gid[j]) : 0ull;
+	if (tid < S)
+		s_fill[tid] = min(fl, cap);
+	__syncthreads();
+	const uint16_t *base = a.pbuf + (uint64_t)p * S * cap;
+	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+	auto add4 = [&](u32x2 v, uint32_t i0, uint32_t np) {
+#pragma unroll
+		for (uint32_t c = 0; c < 2; c++) {
+			if (i0 + 2 * c < np)
+				atomicAdd(&hist[v[c] & 0xffff], 1u);
+			if (i0 + 2 * c + 1 < np)
+				atomicAdd(&hist[v[c] >> 16], 1u);
+		}
+	};
+	for (uint32_t s0 = w; s0 < S; s0 += NWV * U) {
+		u32x2 v[U];
+#pragma unroll
+		for (uint32_t u = 0; u < U; u++) {
+			const uint32_t sl = s0 + u * NWV;
+			const u32x2 *e = (const u32x2 *)(base + (uint64_t)sl * cap);
+			v[u] = sl < S ? __builtin_nontemporal_load(e + lane) : u32x2{ 0, 0 };
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < U; u++) {
+			const uint32_t sl = s0 + u * NWV;
+			add4(v[u], lane * 4, sl < S ? s_fill[sl] : 0u);
+		}
+		// (a fuller slice: the rest)
+#pragma unroll
+		for (uint32_t u = 0; u < U; u++) {
+			const uint32_t sl = s0 + u * NWV;
+			const uint32_t np = sl < S ? s_fill[sl] : 0u;
+			const u32x2 *e = (const u32x2 *)(base + (uint64_t)sl * cap);
+			for (uint32_t i = 256 + lane * 4; i < np; i += 256)
+				add4(__builtin_nontemporal_load(e + i / 4), i, np);
+		}
+	}
+	__syncthreads();
+#pragma unroll
+	for (uint32_t j = 0; j < J; j++) {
+		const uint32_t k = tid + j * LC_THREADS;
+		if (gid[j] != CT_NONE && hist[k])
+			*global_counter(a, gid[j]) = val[j] + hist[k];
 	}
 }
 

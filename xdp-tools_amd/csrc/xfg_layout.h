@@ -84,6 +84,7 @@
 #define XFG_DCNT_MAX      4096u   /* direct LDS counters (16 KiB) */
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
 #define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
+#define XFG_LOG_SLICES_MAX 1024u  /* slices per partition: classify workgroups */
 
 
 /* Per-hash-map descriptor passed to the kernel by value. */
@@ -142,12 +143,16 @@ struct xfg_kargs {
 	uint32_t dcnt;
 	/* Hit log of the pipelined kernels (tlog NULL = no log): per-wave
 	 * regions of defer_cap counter identities; partition-major buffer of
-	 * XFG_LOG_PARTS x pcap entries with fills pfill[]; the count kernel's
-	 * LDS histogram has log_hist entries (xfg_kernels.hip, HitLog). */
+	 * XFG_LOG_PARTS x pslices slices of pcap entries, slice (p, b) owned by
+	 * classify workgroup b (pslices = the classify grid), its entry count in
+	 * pfill[p * pslices + b] (written, not accumulated: no reservation
+	 * atomics); the count kernel's LDS histogram has log_hist entries
+	 * (xfg_kernels.hip, HitLog). */
 	uint32_t *tlog;
-	uint32_t *pbuf;
+	uint16_t *pbuf;               /* local indices (log_local: the partition implied) */
 	uint32_t *pfill;
 	uint32_t pcap;
+	uint32_t pslices;
 	uint32_t log_hist;
 	/* Pipelined kernel: deferred packets, defer_cap entries per wave */
 	uint32_t *defer;
