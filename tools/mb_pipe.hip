@@ -411,6 +411,10 @@ int main(int argc, char **argv)
 		run<3, 1>(nm, b, pc, ncu, e0, e1, bytes);
 		snprintf(nm, sizeof nm, "coal:%s", c.name);
 		run<0, 1>(nm, b, pc, ncu, e0, e1, bytes);
+		snprintf(nm, sizeof nm, "lane:%s", c.name);
+		run<1, 1>(nm, b, pc, ncu, e0, e1, bytes);
+		snprintf(nm, sizeof nm, "lane9:%s", c.name);
+		run<2, 1>(nm, b, pc, ncu, e0, e1, bytes);
 	}
 	return 0;
 }

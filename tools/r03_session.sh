@@ -6,6 +6,13 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"; mkdir -p "$OUT"
 TAG=${1:-s}
 export PYTHONUNBUFFERED=1
+if [ -n "$MB" ]; then
+  for m in $MB; do
+    timeout -k 10 300 ./tools/$m > "$OUT/${m}_$TAG.log" 2>&1
+    rc=$?; echo "$m rc=$rc"; cat "$OUT/${m}_$TAG.log" | cut -c1-200
+    [ $rc -eq 0 ] || exit $rc
+  done
+fi
 if [ -n "$TESTS" ]; then
   timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu $TESTS \
     > "$OUT/pytest_$TAG.log" 2>&1

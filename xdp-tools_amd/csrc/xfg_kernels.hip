@@ -1411,16 +1411,20 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	hipError_t e;
 	switch (prog_features) {
+#ifndef XFG_AB_C3   /* (A/B variant libraries: only xdpfilt_dny_all) */
 	case F_UDP | F_DENY:              e = launch_feat<F_UDP | F_DENY>(*a, grid, s); break;
 	case F_TCP | F_DENY:              e = launch_feat<F_TCP | F_DENY>(*a, grid, s); break;
 	case F_IPV4 | F_IPV6 | F_DENY:    e = launch_feat<F_IPV4 | F_IPV6 | F_DENY>(*a, grid, s); break;
 	case F_ETH | F_DENY:              e = launch_feat<F_ETH | F_DENY>(*a, grid, s); break;
+#endif
 	case XFG_ALL | F_DENY:            e = launch_feat<XFG_ALL | F_DENY>(*a, grid, s); break;
+#ifndef XFG_AB_C3
 	case F_UDP | XFG_ALLOW:           e = launch_feat<F_UDP | XFG_ALLOW>(*a, grid, s); break;
 	case F_TCP | XFG_ALLOW:           e = launch_feat<F_TCP | XFG_ALLOW>(*a, grid, s); break;
 	case F_IPV4 | F_IPV6 | XFG_ALLOW: e = launch_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(*a, grid, s); break;
 	case F_ETH | XFG_ALLOW:           e = launch_feat<F_ETH | XFG_ALLOW>(*a, grid, s); break;
 	case XFG_ALL | XFG_ALLOW:         e = launch_feat<XFG_ALL | XFG_ALLOW>(*a, grid, s); break;
+#endif
 	default:
 		return -22; /* -EINVAL */
 	}
@@ -1479,16 +1483,20 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 extern "C" int xfg_classify_occupancy(uint32_t prog_features, int kind, uint32_t window, size_t dyn)
 {
 	switch (prog_features) {
+#ifndef XFG_AB_C3   /* (A/B variant libraries: only xdpfilt_dny_all) */
 	case F_UDP | F_DENY:              return occupancy_feat<F_UDP | F_DENY>(kind, window, dyn);
 	case F_TCP | F_DENY:              return occupancy_feat<F_TCP | F_DENY>(kind, window, dyn);
 	case F_IPV4 | F_IPV6 | F_DENY:    return occupancy_feat<F_IPV4 | F_IPV6 | F_DENY>(kind, window, dyn);
 	case F_ETH | F_DENY:              return occupancy_feat<F_ETH | F_DENY>(kind, window, dyn);
+#endif
 	case XFG_ALL | F_DENY:            return occupancy_feat<XFG_ALL | F_DENY>(kind, window, dyn);
+#ifndef XFG_AB_C3
 	case F_UDP | XFG_ALLOW:           return occupancy_feat<F_UDP | XFG_ALLOW>(kind, window, dyn);
 	case F_TCP | XFG_ALLOW:           return occupancy_feat<F_TCP | XFG_ALLOW>(kind, window, dyn);
 	case F_IPV4 | F_IPV6 | XFG_ALLOW: return occupancy_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(kind, window, dyn);
 	case F_ETH | XFG_ALLOW:           return occupancy_feat<F_ETH | XFG_ALLOW>(kind, window, dyn);
 	case XFG_ALL | XFG_ALLOW:         return occupancy_feat<XFG_ALL | XFG_ALLOW>(kind, window, dyn);
+#endif
 	default:                          return 1;
 	}
 }
