@@ -44,7 +44,10 @@ def fmix32(h):
 QT_SEED = 0x5eed1234 ^ 0x51ed2701
 
 
-def qt_bucket(keys_u8, bits=17):
+QT_BITS, QT_SLOTS = 17, 16    # xfg_layout.h: 2^17 buckets of 16 entries (small maps)
+
+
+def qt_bucket(keys_u8, bits=QT_BITS):
     k = np.ascontiguousarray(keys_u8, np.uint8).reshape(-1, 4).view("<u4").reshape(-1)
     return fmix32(k ^ np.uint32(QT_SEED)) >> np.uint32(32 - bits)
 
@@ -117,10 +120,11 @@ def test_qt_zero_key_and_ports(G):
 
 
 def test_qt_overflowing_bucket(G):
-    """20 rules homed in one index bucket (15 fit): the 5 spilled keys and
-    every miss homed there are decided by the canonical table (deferred)."""
+    """20 rules homed in one index bucket (15 fit beside the overflow
+    marker): the 5 spilled keys and every miss homed there are decided by
+    the canonical table (deferred)."""
     rng = np.random.default_rng(5)
-    cand = rng.integers(0, 2**32, 1 << 22, dtype=np.uint64).astype(np.uint32)
+    cand = rng.integers(0, 2**32, 1 << 23, dtype=np.uint64).astype(np.uint32)
     cu8 = cand.view(np.uint8).reshape(-1, 4)
     b = qt_bucket(cu8)
     tgt = np.argmax(np.bincount(b))

@@ -34,6 +34,7 @@
 //
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "xfg_layout.h"
 
@@ -916,8 +917,10 @@ template <int NW>
 __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t *s_n,
 					      const uint32_t *s_hist, uint32_t *s, int tid)
 {
+	// (a chunk: whole entries per thread, at most LOG_CHUNK)
 	constexpr int NTH = 64 * NW, K = LOG_CHUNK / NTH;
-	static_assert(LOG_CHUNK % NTH == 0, "chunk: whole entries per thread");
+	constexpr uint32_t CH = K * NTH;
+	static_assert(K >= 1, "chunk: at least one entry per thread");
 	const int nthr = NTH;
 	uint32_t *const s_h = s;                         // histogram, then the chunk's counts
 	uint32_t *const s_cur = s + 2 * XFG_LOG_PARTS;   // entries written per partition
@@ -951,7 +954,7 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 		return;
 #endif
 	// the NW regions as one sequence (entry e of region w at pre[w] + e),
-	// cut into chunks of LOG_CHUNK: runs of about LOG_CHUNK / 256 entries
+	// cut into chunks of CH: runs of about CH / 256 entries
 	uint32_t pre[NW + 1];
 	pre[0] = 0;
 #pragma unroll
@@ -978,8 +981,8 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 	};
 	if (total)
 		fetch(0);
-	for (uint32_t c0 = 0; c0 < total; c0 += LOG_CHUNK) {
-		const uint32_t cn = min(LOG_CHUNK, total - c0);
+	for (uint32_t c0 = 0; c0 < total; c0 += CH) {
+		const uint32_t cn = min(CH, total - c0);
 		// rank each entry within its partition
 #pragma unroll
 		for (int j = 0; j < K; j++)
@@ -1012,8 +1015,8 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 		for (int j = 0; j < K; j++)
 			if (g[j] != CT_NONE)
 				s_srt[s_off[log_part(g[j])] + rk[j]] = g[j];
-		if (c0 + LOG_CHUNK < total)
-			fetch(c0 + LOG_CHUNK);
+		if (c0 + CH < total)
+			fetch(c0 + CH);
 		lds_barrier();
 		for (uint32_t t = tid; t < cn; t += nthr) {
 			const uint32_t x = s_srt[t], p = log_part(x);
@@ -1325,6 +1328,19 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	}
 }
 
+template <uint32_t FEAT, bool L16>
+void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
+{
+	if (a.window <= 64 && a.dense)
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+	else if (a.window <= 64)
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+	else if (a.dense)
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+	else
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+}
+
 template <uint32_t FEAT>
 hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 {
@@ -1356,14 +1372,10 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 			if (a.km == 1 && a.qt) {
 				// the quotient index: one bucket read per packet
 				done = true;
-				if (a.window <= 64 && a.dense)
-					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
-				else if (a.window <= 64)
-					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false>), dim3(grid), dim3(PIPE_THREADS(64)), dl, s, a);
-				else if (a.dense)
-					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
+				if (a.lens_u16)
+					launch_pipeq<FEAT, true>(a, grid, dl, s);
 				else
-					hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false>), dim3(grid), dim3(PIPE_THREADS(128)), dl, s, a);
+					launch_pipeq<FEAT, false>(a, grid, dl, s);
 			} else if (a.km == 1) {
 				done = true;
 				if (a.window <= 64 && a.dense)
@@ -1463,8 +1475,8 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 		} else if (kind == 5) {
 			done = true;
 			e = window <= 64
-				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true>, PIPE_THREADS(64), dyn)
-				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false>, PIPE_THREADS(128), dyn);
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true>, QT_THREADS(64), dyn)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true>, QT_THREADS(128), dyn);
 		}
 	}
 	if (done)
@@ -1506,6 +1518,8 @@ extern "C" int xfg_classify_threads(int kind, uint32_t window)
 {
 	if (kind == 4)
 		return 256;   // the split parse pass (diagnostics build)
+	if (kind == 5)
+		return window <= 64 ? QT_THREADS(64) : QT_THREADS(128);
 	return kind >= 1 ? (window <= 64 ? PIPE_THREADS(64) : PIPE_THREADS(128)) : TILE;
 }
 

@@ -40,16 +40,25 @@
  * the filter when stale bits accumulate.
  *
  * Quotient index ("QT", xfg_table.h xfg_qt): a derived, read-only index of
- * the IPv4 map that answers a lookup with ONE random 32-byte read and no
- * prefilter, for the pipelined IPv4-key kernel when exactly one lookup
- * direction can hit.  h = xfg_qt_hash(key) is a bijection of the 32-bit key,
- * so (bucket = h >> (32 - bits), remainder = h's low 32 - bits <= 15 bits)
- * identifies the key exactly.  A bucket is 16 u16: entry 0 = count (bits
- * 0-3) | overflow (bit 15: a key homed here did not fit; a miss here is
- * decided by the canonical table instead), entries 1..count = remainder |
- * live << 15 (live: the key's flags carry the one live mask).  QT slot
- * bucket * 15 + entry - 1 maps back to the canonical slot through
- * trans[] (the count kernel's job).
+ * the IPv4 map that answers a lookup with ONE random 32-byte read (two
+ * 16-byte loads of one line by the packet's own lane) and no prefilter, for
+ * the pipelined IPv4-key kernel when exactly one lookup direction can hit.
+ * h = xfg_qt_hash(key) is a bijection of the 32-bit key, so (bucket = h >>
+ * (32 - bits), remainder = h's low 32 - bits <= 15 bits) identifies the key
+ * exactly.  A bucket is 16 u16 entries filled in order: 0 = empty, else
+ * 0x8000 | remainder.  A bucket that more than 16 keys home in holds 15 of
+ * them and, as entry 15, the overflow marker 0x0001 (no lookup's 0x8000 |
+ * remainder equals it): a miss there is decided by the canonical table
+ * instead (the kernel defers it); a miss in a bucket of exactly 16 is
+ * final.  Only keys whose flags carry the one live mask are
+ * indexed: any other key cannot hit this lookup, exactly as an absent one.
+ * QT slot bucket * 16 + entry maps back to the canonical slot through
+ * trans[] (the count kernel's job).  What a tile's lookups cost is set by
+ * the random LINES they touch (tools/mb_vm.hip, profiles/r03_mb_vm*.log:
+ * 64 lines per 64-packet tile add ~0.25 ms per 2^26 packets to the frame
+ * stream, 32 lines 0.07, 16 lines 0.02; a table of 0.5-4 MB the same), so
+ * a bucket is one line's worth, and 16 entries at < 8 keys per bucket
+ * keep the deferred share near 0.3 % of the misses.
  *
  * filter_ports (PERCPU_ARRAY[65536], :67-73) is dense: flags[65536] u8 and
  * hits[65536] u64 indexed by the raw big-endian port value, plus a 65536-bit
@@ -76,10 +85,12 @@
 
 #define XFG_BLOOM_K       4u
 
-#define XFG_QT_SLOTS      15u     /* entries per 32-byte QT bucket */
+#define XFG_QT_SLOTS      16u     /* entries per 32-byte QT bucket */
 #define XFG_QT_BUCKET     32u
 #define XFG_QT_MIN_BITS   17u     /* remainders of at most 15 bits */
-#define XFG_QT_OVF        0x8000u
+#define XFG_QT_LOAD       8u      /* fewer keys per bucket than this on average */
+#define XFG_QT_USED       0x8000u /* an occupied entry */
+#define XFG_QT_OVF_MARK   0x0001u /* entry 15: the bucket overflowed */
 
 #define XFG_DCNT_MAX      4096u   /* direct LDS counters (16 KiB) */
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */

@@ -50,6 +50,16 @@ constexpr uint32_t A_DEFER = 6;
 
 #define PIPE_WAVES(W) ((W) <= 64 ? 8 : 4)
 #define PIPE_THREADS(W) (64 * PIPE_WAVES(W))
+// the quotient-index kernel (xfg_pipeq.hip): waves per workgroup (two
+// workgroups per CU).  10 (5 waves per SIMD, 96 VGPRs) sped the stream and
+// parse up 4 % but the whole classify down 4 %: more requests in flight
+// than the CU's vector memory path serves (profiles/r03_qt_waves_ab.log)
+#ifndef XFG_QT_NW
+#define XFG_QT_NW 8
+#endif
+#define QT_WAVES(W) ((W) <= 64 ? XFG_QT_NW : 4)
+#define QT_THREADS(W) (64 * QT_WAVES(W))
+#define QT_MINW(W) ((W) <= 64 ? (2 * XFG_QT_NW + 3) / 4 : 2)
 
 // Key descriptor: kind | mask << 2 | zero << 4 | byte offset << 5.
 __device__ __forceinline__ uint32_t kd_kind(uint32_t d) { return d & 3; }
@@ -726,7 +736,11 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	const bool arp = et == 0x0608;
 	// IPv4 (__parse_iphdr, frags ok, no version check): ihl 5 keeps L4 at 34
 	const bool s4 = len < 34;
-	const bool ihl5 = ((d3 >> 16) & 0xf) == 5;
+	const uint32_t ihl = (d3 >> 16) & 0xf;
+	const bool ihl5 = ihl == 5;
+	// (parsing_helpers.h:215: a header past the frame is a parse failure,
+	// decided here; any other ihl but 5 moves L4: deferred)
+	const bool ihlx = 14 + ihl * 4 > len;
 	const uint32_t proto = d5 >> 24;
 	const bool u4 = (FEAT & F_UDP) && proto == 17, t4 = (FEAT & F_TCP) && proto == 6;
 	const uint32_t ulen4 = ((d9 >> 8) & 0xff00) | (d9 >> 24);
@@ -745,8 +759,8 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	const bool t6far = (W < 68) & t6 & (len >= 74);   // doff at byte 66: past the window
 	const bool ab6 = (u6 & ((len < 62) | (ulen6 < 8))) | (t6 & ((len < 74) | (54 + doff6 * 4 > len)));
 	Parse4 r;
-	r.defer = !runt & (vlan | arp | (is4 & !s4 & !ihl5) | (is6 & !s6 & (ext | t6far)));
-	const bool sip = (is4 & s4) | (is6 & s6);          // short IP header
+	r.defer = !runt & (vlan | arp | (is4 & !s4 & !ihl5 & !ihlx) | (is6 & !s6 & (ext | t6far)));
+	const bool sip = (is4 & (s4 | ihlx)) | (is6 & s6);   // short IP header
 	const bool sl4 = (is4 & !s4 & ab4) | (is6 & !s6 & ab6);
 	r.abort_at = pick(runt, ST_ETH, pick(sip, ST_IP, pick(sl4, ST_L4, NST)));
 	const uint32_t l4 = pick(is4, pick(u4, 17u, pick(t4, 6u, 0u)), pick(is6, pick(u6, 17u, pick(t6, 6u, 0u)), 0u));

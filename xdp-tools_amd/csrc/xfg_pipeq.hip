@@ -5,15 +5,19 @@
 // xfg_pipeline.hip, whose parse (parse_bf), port probe and packing it uses.
 //
 // Why: the reference program's map lookup (CHECK_MAP,
-// xdp-filter/xdpfilt_prog.h:56-64) is a random access per packet.  On
-// gfx950 random requests cost on top of the frame stream (measured:
-// tools/mb_pipe.hip, profiles/r03_mb_*): a prefilter word plus a 64-byte
-// line for half the packets from the 8.9 MB canonical table took 1.16-1.19
-// ms per 2^26 packets, one 32/64-byte bucket per packet from a <= 4 MB
-// table 0.95.  The quotient index is that table: 2^bits buckets of 15
-// entries, a bijective key hash so that a bucket's 15-bit remainders
-// identify their keys exactly, and the one live direction's mask bit per
-// entry -- so a lookup is ONE random 32-byte read, no prefilter hop.
+// xdp-filter/xdpfilt_prog.h:56-64) is a random access per packet, and on
+// gfx950 what a tile's random reads cost beside the frame stream is set by
+// the distinct LINES they touch: 64 random lines per 64-packet tile add
+// ~0.25 ms per 2^26 packets, 32 lines 0.07, 16 lines 0.02, from a table of
+// 0.5 to 4 MB alike (tools/mb_vm.hip, profiles/r03_mb_vm*.log).  The
+// quotient index is the IPv4 map reduced to one 32-byte bucket per lookup
+// -- 2^bits buckets of 16 entries, a bijective key hash so that a bucket's
+// 15-bit remainders identify their keys exactly, only keys that carry the
+// one live direction's mask -- read as two 16-byte halves by two lanes of
+// ONE load instruction (32 packets' buckets per instruction, so each line
+// is looked up once) and moved to the packet's lane by v_permlane32_swap:
+// no prefilter hop, no LDS.  Lanes without a lookup load bucket 0 (one
+// shared line), so they add no lines.
 //
 // Used when exactly one IPv4 lookup direction can hit (flag census), every
 // device carries the same flags, and the map is large (xfg_ctx.c
@@ -22,21 +26,22 @@
 // go to the deferred list and the canonical table (classify_staged).
 //
 // Per wave, iteration k works on three tiles of 64 packets:
-//   R  tile k-1's buckets (LDS-DMA'd by L last iteration): match -> verdict
+//   R  tile k-1's buckets (loaded by L last iteration): match -> verdict
 //   W  tile k-1's verdict stores, counters, stats, deferrals
 //   S  tile k's windows (loaded two iterations ago) into the LDS rows
 //   P  parse tile k, hash its key, plan its fallback (ports from LDS)
-//   L  tile k's buckets, LDS-DMA'd into the rows (two lanes a bucket)
-//   I  tile k+2's windows and lengths issued
+//   L  tile k's buckets: two dwordx4 loads, 32 packets' buckets each
+//   I  tile k+2's windows and length issued
 // One wait per iteration, at its top: everything but the newest tile's
-// CPP + 2 loads.
+// CPP + 1 loads.  Every iteration issues the same loads (a lane without a
+// lookup loads bucket 0), so the count is fixed.
 namespace {
 
-template <uint32_t FEAT, int W, bool DENSE>
-__global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_kernel(const xfg_kargs a)
+template <uint32_t FEAT, int W, bool DENSE, bool L16>
+__global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
 	static_assert((FEAT & F_IPV4) != 0, "IPv4-key mode needs the IPv4 feature");
-	constexpr int NW = PIPE_WAVES(W);
+	constexpr int NW = QT_WAVES(W);
 	constexpr int NT = 64 * NW;
 	constexpr int CPP = W / 16;
 	constexpr int ROWDW = W / 4 + 1;
@@ -44,7 +49,6 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	constexpr uint32_t QTAG = 0x80000000u;   // tag bit: a QT slot (hit log), not a counter identity
-	static_assert(NW * 64 * ROWDW * 4 >= 64 * XFG_QT_BUCKET * NW, "buckets fit the rows");
 	__shared__ uint32_t win[NW * 64 * ROWDW > LOG_SCRATCH ? NW * 64 * ROWDW : LOG_SCRATCH];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
 	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB : 1];
@@ -53,6 +57,14 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 	__shared__ unsigned long long s_stats[6];
 	extern __shared__ uint32_t s_dyn[];
 
+#ifdef XFG_DIAG
+	// (diagnostics: 1 no counting, 2 no bucket loads, 8 no verdict stores,
+	// 16 no workgroup-end partition, 2048 no deferred packets, 4096 hits as
+	// memory-side atomics into scratch instead of the hit log -- results wrong)
+	const uint32_t dg = a.diag;
+#else
+	constexpr uint32_t dg = 0;
+#endif
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 	// the index, in scalar registers
@@ -90,9 +102,14 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 		const bool ps = pslot < XFG_PORT_TAB;
 		const bool dc = !q & (tag < a.dcnt);
 		const uint32_t qs = tag & ~QTAG;
-		log_append(tregion, tn, pick(q, qs, CT_NONE), lane);
-		if (q)
-			atomicAdd(&s_lh[log_part(qs)], 1u);
+		if (dg & 4096) {   // (diagnostics: a memory-side atomic per hit into scratch)
+			if (q)
+				atomicAdd(reinterpret_cast<uint32_t *>(a.pbuf) + qs, 1u);
+		} else {
+			log_append(tregion, tn, pick(q, qs, CT_NONE), lane);
+			if (q)
+				atomicAdd(&s_lh[log_part(qs)], 1u);
+		}
 		if constexpr (PORTS)
 			if (ps)
 				atomicAdd(&s_pcnt[pslot], 1u);
@@ -115,80 +132,108 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 	};
 	uint32_t ndef = 0;
 
-	// windows + lengths of tile t (clamped to the last tile): CPP + 2 loads,
-	// always issued (as xfg_pipe4_kernel's)
-	const bool l16 = a.lens_u16 != 0;
-	const uint32_t lsh = l16 ? 1u : 2u;
+	// windows + lengths of tile t (clamped to the last tile): CPP + 1 loads,
+	// always issued
+	// (the length width is a template parameter: one load of a fixed kind,
+	// so the compiler's wait counts stay exact across the loop)
+	constexpr uint32_t lsh = L16 ? 1u : 2u;
+	typedef typename std::conditional<L16, uint16_t, uint32_t>::type len_t;
 	const uint64_t lb = rfl64((uint64_t)(uintptr_t)a.lens);
-	auto issue = [&](uint32_t t, u32x4 (&pre)[CPP], uint16_t (&plen)[2]) {
+	// (a whole tile -- every one but a ragged last -- takes a uniform branch
+	// with no per-lane clamps: a scalar tile base and per-lane offsets that
+	// do not change from tile to tile; the same loads either way)
+	auto issue = [&](uint32_t t, u32x4 (&pre)[CPP], len_t &plen) {
 		t = t < nt ? t : nt - 1;
 		const uint32_t base = t * 64;
 		const uint32_t rem = n - base >= 64 ? 64u : n - base;
+		if (rem == 64) {
+			const uint8_t *tb = a.data + (uint64_t)base * (DENSE ? W : a.stride);
 #pragma unroll
-		for (int it = 0; it < CPP; it++) {
-			const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
-			const uint32_t q = pk < rem ? pk : 0u;
-			const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + (q * CPP + sub)
-						 : reinterpret_cast<const u32x4 *>(a.data + (uint64_t)(base + q) * a.stride + sub * 16);
-			pre[it] = __builtin_nontemporal_load(src);
+			for (int it = 0; it < CPP; it++) {
+				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
+				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
+							 : reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
+				pre[it] = __builtin_nontemporal_load(src);
+			}
+			plen = *reinterpret_cast<const __attribute__((address_space(1))) len_t *>(
+				lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
+		} else {
+#pragma unroll
+			for (int it = 0; it < CPP; it++) {
+				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
+				const uint32_t q = pk < rem ? pk : 0u;
+				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + (q * CPP + sub)
+							 : reinterpret_cast<const u32x4 *>(a.data + (uint64_t)(base + q) * a.stride + sub * 16);
+				pre[it] = __builtin_nontemporal_load(src);
+			}
+			const uint64_t la = lb + ((uint64_t)(base + ((uint32_t)lane < rem ? lane : 0u)) << lsh);
+			plen = *reinterpret_cast<const __attribute__((address_space(1))) len_t *>(la);
 		}
-		const uint64_t la = lb + ((uint64_t)(base + ((uint32_t)lane < rem ? lane : 0u)) << lsh);
-		plen[0] = *reinterpret_cast<const __attribute__((address_space(1))) uint16_t *>(la);
-		plen[1] = *reinterpret_cast<const __attribute__((address_space(1))) uint16_t *>(la + (lsh - 1) * 2);
 	};
 
 	auto pk3 = [](uint32_t act, uint32_t ps, uint32_t len) { return act | ps << 3 | len << 15; };
 	auto pk_act = [](uint32_t p) { return p & 7; };
 	auto pk_ps = [](uint32_t p) { return (p >> 3) & 0xfff; };
 	auto pk_len = [](uint32_t p) { return p >> 15; };
-	// P -> R (tile k-1): remainder, bucket, fallback
-	uint32_t r_rem = 0, r_b = 0, r_pk = pk3(A_NONE, XFG_PORT_TAB, 0), r_tag = CT_NONE;
+	// P -> R (tile k-1): entry to find (USED | remainder), bucket, its
+	// 32 bytes (L -> R), fallback
+	uint32_t r_key = 0, r_b = 0, r_pk = pk3(A_NONE, XFG_PORT_TAB, 0), r_tag = CT_NONE;
 	bool r_sel = false;
+	u32x4 bk0 = { 0, 0, 0, 0 }, bk1 = { 0, 0, 0, 0 };
 
-	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], uint16_t (&curlen)[2]) {
+	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen) {
 		const uint32_t tP = first + k * step;
 		const bool vP = tP < nt;
 		const bool vR = k >= 1 && tP - step < nt;
-		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 2) & 15) | (((CPP + 2) >> 4) << 14));
-		asm volatile("" ::: "memory");   // (the LDS-DMA'd buckets: read only after the wait)
+		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
+		// (the length is used from here on: without this the compiler
+		// rotates its zero-extension to the previous iteration's end, where
+		// it waits for the load -- and every older one -- early)
+		asm volatile("" : "+v"(curlen));
 
+		PMARK("R");
 		// ---- R: tile k-1's bucket -> CHECK_MAP (xdpfilt_prog.h:56-64)
 		const uint32_t r_act = pk_act(r_pk), r_ps = pk_ps(r_pk), w_len = pk_len(r_pk);
 		uint32_t w_act = A_NONE, w_tag = CT_NONE, w_ps = r_ps;
 		if (vR) {
-			// packet p's bucket: halves at (p>>5)*1024 + (j*32 + (p&31))*16 bytes
-			const u32x4 *bp4 = reinterpret_cast<const u32x4 *>(rows) + (lane >> 5) * 64 + (lane & 31);
-			const u32x4 h0 = bp4[0], h1 = bp4[32];
-			const uint32_t w[8] = { h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w };
-			const uint32_t rr = r_rem | (r_rem << 16);
-			uint32_t mm = 0, lv = 0;
+			// 16 entries, filled in order; keys are unique, so at most one
+			// matches.  A miss in a bucket marked overflowed may be a key
+			// that did not fit: the canonical table decides it (deferred).
+			const uint32_t q = r_key;
+			// the halves to their packet's lane (see L): lane i < 32 holds
+			// half 0 of packet i in bk0 and half 1 of packet i in lane
+			// i + 32 of bk0; lanes i + 32 likewise in bk1 for packet 32 + i
+			uint32_t w[8];
+#pragma unroll
+			for (int c = 0; c < 4; c++) {
+				const auto sw = __builtin_amdgcn_permlane32_swap(bk0[c], bk1[c], false, false);
+				w[c] = sw[0];
+				w[4 + c] = sw[1];
+			}
+			bool found = false;
+			uint32_t ix = 0;
 #pragma unroll
 			for (int i = 0; i < 8; i++) {
-				// zero 15-bit halves of (w ^ rr): bit 15 / 31 of ~t (no borrow
-				// crosses the halves: each is at least 0x7fff after the -1)
-				const uint32_t z = (w[i] ^ rr) & 0x7fff7fffu;
-				const uint32_t t = ~((z | 0x80008000u) - 0x00010001u) & 0x80008000u;
-				const uint32_t v = t >> 15, l = (w[i] & 0x80008000u) >> 15;
-				mm |= ((v | (v >> 15)) & 3u) << (2 * i);
-				lv |= ((l | (l >> 15)) & 3u) << (2 * i);
+				const bool lo = (w[i] & 0xffffu) == q, hi = (w[i] >> 16) == q;
+				found |= lo | hi;
+				ix = pick(lo, 2u * i, ix);
+				ix = pick(hi, 2u * i + 1, ix);
 			}
-			const uint32_t cntq = w[0] & 15;
-			mm &= ((2u << cntq) - 2u) & 0xfffeu;   // entries 1..count
-			const bool found = r_sel & (mm != 0);
-			const bool hit = found & ((mm & lv) != 0);
-			const bool defer = r_sel & !found & ((w[0] & XFG_QT_OVF) != 0);
-			const uint32_t slot = r_b * XFG_QT_SLOTS + (uint32_t)__builtin_ctz(mm | 0x10000u) - 1;
-			w_act = pick(hit, HIT, pick(defer, A_DEFER, r_act));
-			w_tag = pick(hit, QTAG | slot, pick(defer, CT_NONE, r_tag));
-			w_ps = pick(hit | defer, XFG_PORT_TAB, r_ps);
+			found &= r_sel;
+			const bool defer = r_sel & !found & ((w[7] >> 16) == XFG_QT_OVF_MARK);
+			const uint32_t slot = r_b * XFG_QT_SLOTS + ix;
+			w_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
+			w_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, r_tag));
+			w_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
 		}
 
+		PMARK("W");
 		// ---- W: verdicts, counters, stats, deferrals of tile k-1
 		if (vR) {
 			const uint32_t gi = (tP - step) * 64 + lane;
-			if (w_act <= A_PASS)
+			if (w_act <= A_PASS && !(dg & 8))
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
-			count(w_tag, w_ps);
+			count((dg & 1) ? CT_NONE : w_tag, (dg & 1) ? XFG_PORT_TAB : w_ps);
 			stat(w_act, w_len);
 			const unsigned long long dm = __ballot(w_act == A_DEFER);
 			if (dm) {
@@ -199,8 +244,11 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 			}
 		}
 
-		// ---- S: tile k's windows into the rows (past the batch's end:
-		// zeroes), lengths clamped to the stride
+		PMARK("S");
+		// ---- S: tile k's windows into the rows, lengths clamped to the
+		// stride (rows past the batch's end hold a copy of the tile's first
+		// packet: those lanes are not valid, nothing of theirs is stored or
+		// counted)
 		uint32_t len = 0;
 		if (vP) {
 			const uint32_t rem = n - tP * 64 >= 64 ? 64u : n - tP * 64;
@@ -209,20 +257,18 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 			for (int it = 0; it < CPP; it++) {
 				const int c = it * 64 + lane;
 				const int pk = c / CPP, sub = c % CPP;
-				const bool ok = (uint32_t)pk < rem;
 				uint32_t *dst = &rows[pk * ROWDW + sub * 4];
-				dst[0] = ok ? cur[it].x : 0u;
-				dst[1] = ok ? cur[it].y : 0u;
-				dst[2] = ok ? cur[it].z : 0u;
-				dst[3] = ok ? cur[it].w : 0u;
+				dst[0] = cur[it].x;
+				dst[1] = cur[it].y;
+				dst[2] = cur[it].z;
+				dst[3] = cur[it].w;
 			}
-			const uint32_t l = l16 ? (uint32_t)curlen[0] : (uint32_t)curlen[0] | (uint32_t)curlen[1] << 16;
-			len = (uint32_t)lane < rem ? min(l, a.stride) : 0u;
+			len = (uint32_t)lane < rem ? min((uint32_t)curlen, a.stride) : 0u;
 			__builtin_amdgcn_wave_barrier();
 		}
 
+		PMARK("P");
 		// ---- P: parse tile k, hash its key, plan its fallback
-		bool lsel = false;
 		if (vP) {
 			const uint32_t gi = tP * 64 + lane;
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
@@ -230,10 +276,9 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 			const bool kok = valid & !r.defer & r.v4ok & klive;
 			const uint32_t key = dlive ? r.k4a : r.k4b;
 			const uint32_t h = xfg_qt_hash(key, qseed);
-			r_b = h >> rsh;
-			r_rem = h & rmask;
+			r_b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
+			r_key = XFG_QT_USED | (h & rmask);
 			r_sel = kok;
-			lsel = kok;
 			uint32_t fa = pick(r.abort_at != NST, A_ABORTED, MISS), ft = CT_NONE, fs = XFG_PORT_TAB;
 			if constexpr (PORTS) {
 				if (a.port_count) {
@@ -265,30 +310,24 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 			r_tag = pick(valid & !r.defer, ft, CT_NONE);
 		} else {
 			r_sel = false;
+			r_b = 0;
 			r_pk = pk3(A_NONE, XFG_PORT_TAB, 0);
 			r_tag = CT_NONE;
 		}
 
-		// ---- L: tile k's buckets LDS-DMA'd into the rows (free once P has
-		// read them): instruction q carries packets 32q..32q+31, lane L the
-		// 16-byte half L >> 5 of packet 32q + (L & 31)'s bucket
-		{
-			const unsigned long long need = __ballot(lsel);
-			if (need) {
-				__builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): P's row reads are done
-				__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-				for (int q = 0; q < 2; q++) {
-					const uint32_t p = q * 32 + (lane & 31);
-					const uint32_t bp = __shfl(r_b, (int)p);
-					if ((need >> p) & 1)
-						__builtin_amdgcn_global_load_lds(
-							(const __attribute__((address_space(1))) void *)(
-								qb + (uint64_t)bp * XFG_QT_BUCKET + (lane >> 5) * 16),
-							(__attribute__((address_space(3))) void *)(rows + q * 256), 16, 0, 0);
-				}
-			}
+		PMARK("L");
+		// ---- L: tile k's buckets: load q carries packets 32q..32q+31, lane
+		// L the 16-byte half L >> 5 of packet 32q + (L & 31)'s bucket, so
+		// both halves of a bucket are in ONE instruction (a line is looked
+		// up once); R moves them to the packet's lane.  Every lane loads
+		// (a fixed count).
+		if (!(dg & 2)) {
+			const auto ab = __builtin_amdgcn_permlane32_swap(r_b, r_b, false, false);
+			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
+			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
+			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
 		}
+		PMARK("I");
 		// ---- tile k+2's windows, last: in flight for two iterations
 		__builtin_amdgcn_sched_barrier(0);
 		issue(tP + 2 * step, cur, curlen);
@@ -296,7 +335,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 	};
 
 	u32x4 preA[CPP], preB[CPP];
-	uint16_t lenA[2] = { 0, 0 }, lenB[2] = { 0, 0 };
+	len_t lenA = 0, lenB = 0;
 	if (nt) {
 		issue(first, preA, lenA);
 		__builtin_amdgcn_sched_barrier(0);
@@ -312,11 +351,8 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 	if (k < iters)
 		iteration(k, preA, lenA);
 
-#ifdef XFG_DIAG
-	// (diagnostics: 2048 skips the deferred packets -- results wrong)
-	if (a.diag & 2048)
+	if (dg & 2048)
 		ndef = 0;
-#endif
 	// the deferred packets: the whole reference walk over the canonical
 	// table (classify_staged), 64 at a time
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
@@ -355,10 +391,8 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeq_
 			for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
 				if (s_pcnt[i])
 					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
-#ifdef XFG_DIAG
-	if (a.diag & 16)   // (diagnostics: no workgroup-end partition -- counts wrong)
+	if (dg & 16)
 		return;
-#endif
 	if (a.tlog)   // (win is free now: the partition scratch)
 		log_partition<NW>(a, s_tn, s_lh, win, tid);
 }

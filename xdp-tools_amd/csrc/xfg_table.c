@@ -243,7 +243,7 @@ void xfg_table_desc(const struct xfg_table *t, struct xfg_tdesc *d)
 uint32_t xfg_qt_bits_for(uint32_t count)
 {
 	uint32_t b = XFG_QT_MIN_BITS;
-	while (b < 30 && ((uint64_t)count >> b) > 8)
+	while (b < 30 && ((uint64_t)count >> b) >= XFG_QT_LOAD)
 		b++;
 	return b;
 }
@@ -280,22 +280,40 @@ int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *fla
 	q->nslots = (uint32_t)ns;
 	q->placed = q->spilled = 0;
 	const uint32_t rbits = 32 - bits, rmask = (1u << rbits) - 1;
+	/* keys homed per bucket first: a bucket that more than XFG_QT_SLOTS
+	 * keys home in holds XFG_QT_SLOTS - 1 of them and the overflow marker */
+	uint8_t *homed = calloc(nb, 1);
+	if (!homed)
+		return -ENOMEM;
 	for (int64_t s = xfg_table_next_slot(t, -1); s >= 0; s = xfg_table_next_slot(t, s)) {
+		if ((flags[s] & live) != live)
+			continue;
+		uint32_t k;
+		xfg_table_slot_key(t, (uint64_t)s, &k);
+		const uint32_t b = xfg_qt_hash(k, seed) >> rbits;
+		if (homed[b] < 255)
+			homed[b]++;
+	}
+	for (int64_t s = xfg_table_next_slot(t, -1); s >= 0; s = xfg_table_next_slot(t, s)) {
+		if ((flags[s] & live) != live)
+			continue;   /* cannot hit this lookup: as absent */
 		uint32_t k;
 		xfg_table_slot_key(t, (uint64_t)s, &k);   /* the wire bytes, as the kernel loads them */
 		const uint32_t h = xfg_qt_hash(k, seed), b = h >> rbits;
-		uint16_t *e = q->img + (uint64_t)b * 16;
-		const uint32_t c = e[0] & 15;
-		if (c == XFG_QT_SLOTS) {   /* full: the canonical table answers this bucket's misses */
-			e[0] |= XFG_QT_OVF;
+		uint16_t *e = q->img + (uint64_t)b * XFG_QT_SLOTS;
+		const uint32_t room = homed[b] > XFG_QT_SLOTS ? XFG_QT_SLOTS - 1 : XFG_QT_SLOTS;
+		uint32_t c = 0;
+		while (c < room && (e[c] & XFG_QT_USED))
+			c++;
+		if (c == room) {   /* the canonical table answers this bucket's misses */
+			e[XFG_QT_SLOTS - 1] = XFG_QT_OVF_MARK;
 			q->spilled++;
 			continue;
 		}
-		const uint32_t lv = (flags[s] & live) == live;
-		e[1 + c] = (uint16_t)((h & rmask) | (lv << 15));
-		e[0] = (uint16_t)((e[0] & XFG_QT_OVF) | (c + 1));
+		e[c] = (uint16_t)(XFG_QT_USED | (h & rmask));
 		q->trans[(uint64_t)b * XFG_QT_SLOTS + c] = (uint32_t)s;
 		q->placed++;
 	}
+	free(homed);
 	return 0;
 }

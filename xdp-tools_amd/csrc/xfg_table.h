@@ -78,19 +78,21 @@ static inline uint64_t xfg_table_img_bytes(const struct xfg_table *t)
 
 /* Quotient index of a table of 4-byte keys (layout: xfg_layout.h).  Built
  * from the table's keys and each slot's flag byte (@flags[slot], the same on
- * every device); entries answer lookups of mask @live.  Returns 0 or
+ * every device); only keys carrying mask @live are entered (the lookups it
+ * answers are of that mask).  Returns 0 or
  * -ENOMEM / -EINVAL (not 4-byte keys). */
 struct xfg_qt {
 	uint32_t bits, seed, live;
 	uint32_t nslots;      /* (1 << bits) * XFG_QT_SLOTS */
-	uint16_t *img;        /* (1 << bits) * 16 entries */
+	uint16_t *img;        /* (1 << bits) * XFG_QT_SLOTS entries */
 	uint32_t *trans;      /* nslots: canonical slot, or ~0u */
 	uint32_t placed, spilled;
 };
 int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *flags,
 		 uint32_t live, uint32_t seed);
 void xfg_qt_free(struct xfg_qt *q);
-/* Bucket bits for @count keys: at most ~8 keys per 15-entry bucket. */
+/* Bucket bits for @count keys: fewer than XFG_QT_LOAD keys per 16-entry
+ * bucket on average (a 1M-key map: 2^17 buckets, 4 MB). */
 uint32_t xfg_qt_bits_for(uint32_t count);
 
 /* Descriptor for the kernel (device pointers filled by the caller). */
