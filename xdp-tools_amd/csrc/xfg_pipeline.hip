@@ -769,7 +769,7 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	r.pdst = pick(is4, d9 & 0xffff, d14 & 0xffff);
 	r.k4a = __builtin_amdgcn_alignbyte(d8, d7, 2);   // daddr 30..33
 	r.k4b = __builtin_amdgcn_alignbyte(d7, d6, 2);   // saddr 26..29
-	r.v4ok = !runt & is4 & !s4;
+	r.v4ok = !runt & is4 & !s4 & !ihlx;
 	return r;
 }
 
