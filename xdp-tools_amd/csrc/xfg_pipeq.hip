@@ -29,12 +29,18 @@
 //   R  tile k-1's buckets (loaded by L last iteration): match -> verdict
 //   W  tile k-1's verdict stores, counters, stats, deferrals
 //   S  tile k's windows (loaded two iterations ago) into the LDS rows
-//   P  parse tile k, hash its key, plan its fallback (ports from LDS)
-//   L  tile k's buckets: two dwordx4 loads, 32 packets' buckets each
+//   L  tile k's key hashed from the row's fixed dwords, its buckets: two
+//      dwordx4 loads, 32 packets' buckets each (before the parse: the
+//      loads gain its duration)
+//   P  parse tile k, plan its fallback (ports from LDS)
 //   I  tile k+2's windows and length issued
 // One wait per iteration, at its top: everything but the newest tile's
 // CPP + 1 loads.  Every iteration issues the same loads (a lane without a
 // lookup loads bucket 0), so the count is fixed.
+#ifndef XFG_QT_EARLY_L
+#define XFG_QT_EARLY_L 1
+#endif
+
 namespace {
 
 template <uint32_t FEAT, int W, bool DENSE, bool L16>
@@ -267,6 +273,31 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			__builtin_amdgcn_wave_barrier();
 		}
 
+#if XFG_QT_EARLY_L
+		PMARK("L");
+		// ---- K + L: the key's hash from the row's fixed dwords and tile
+		// k's bucket loads first, the rest of the parse after them (the
+		// loads gain its duration).  Load q carries packets 32q..32q+31,
+		// lane L the 16-byte half L >> 5 of packet 32q + (L & 31)'s bucket,
+		// so both halves of a bucket are in ONE instruction (a line is
+		// looked up once); R moves them to the packet's lane.  Every lane
+		// loads (a fixed count); one whose frame is not IPv4 loads bucket 0
+		// (a shared line).
+		uint32_t hk = 0, lbk = 0;
+		if (vP) {
+			const uint32_t e3 = myrow[3], e6 = myrow[6], e7 = myrow[7], e8 = myrow[8];
+			const uint32_t key = dlive ? __builtin_amdgcn_alignbyte(e8, e7, 2) : __builtin_amdgcn_alignbyte(e7, e6, 2);
+			hk = xfg_qt_hash(key, qseed);
+			lbk = pick((e3 & 0xffffu) == 0x0008u, hk >> rsh, 0u);
+		}
+		if (!(dg & 2)) {
+			const auto ab = __builtin_amdgcn_permlane32_swap(lbk, lbk, false, false);
+			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
+			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
+			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
+		}
+		__builtin_amdgcn_sched_barrier(0);
+#endif
 		PMARK("P");
 		// ---- P: parse tile k, hash its key, plan its fallback
 		if (vP) {
@@ -274,8 +305,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
 			const bool kok = valid & !r.defer & r.v4ok & klive;
+#if XFG_QT_EARLY_L
+			const uint32_t h = hk;
+#else
 			const uint32_t key = dlive ? r.k4a : r.k4b;
 			const uint32_t h = xfg_qt_hash(key, qseed);
+#endif
 			r_b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
 			r_key = XFG_QT_USED | (h & rmask);
 			r_sel = kok;
@@ -315,6 +350,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			r_tag = CT_NONE;
 		}
 
+#if !XFG_QT_EARLY_L
 		PMARK("L");
 		// ---- L: tile k's buckets: load q carries packets 32q..32q+31, lane
 		// L the 16-byte half L >> 5 of packet 32q + (L & 31)'s bucket, so
@@ -327,8 +363,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
 			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
 		}
+#endif
 		PMARK("I");
 		// ---- tile k+2's windows, last: in flight for two iterations
+		// (issued before the parse instead, the compiler's register
+		// reuse puts waits into R: not kept)
 		__builtin_amdgcn_sched_barrier(0);
 		issue(tP + 2 * step, cur, curlen);
 		__builtin_amdgcn_sched_barrier(0);
