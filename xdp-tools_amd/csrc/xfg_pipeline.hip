@@ -734,6 +734,16 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	const bool is4 = et == 0x0008, is6 = et == 0xdd86;
 	const bool vlan = (et == 0x0081) | (et == 0xa888);
 	const bool arp = et == 0x0608;
+	// a VLAN tag past the frame: parse_ethhdr stops at it (parsing_helpers.h
+	// :121-126) and returns the tag's ethertype -- no IP, no lookups
+	const bool vshort = len < 18;
+	// parse_arphdr (parsing_helpers.h:235-253; ARP is parsed only with the
+	// IPv4 feature, xdpfilt_prog.h:240-261): a short or non-Ethernet/IPv4
+	// ARP header is a parse failure, decided here
+	constexpr bool ARPP = (FEAT & F_IPV4) != 0;
+	bool arpbad = false;
+	if constexpr (ARPP)
+		arpbad = arp & ((len < 42) | ((d3 >> 16) != 0x0100u) | (row[4] != 0x04060008u));
 	// IPv4 (__parse_iphdr, frags ok, no version check): ihl 5 keeps L4 at 34
 	const bool s4 = len < 34;
 	const uint32_t ihl = (d3 >> 16) & 0xf;
@@ -759,8 +769,9 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	const bool t6far = (W < 68) & t6 & (len >= 74);   // doff at byte 66: past the window
 	const bool ab6 = (u6 & ((len < 62) | (ulen6 < 8))) | (t6 & ((len < 74) | (54 + doff6 * 4 > len)));
 	Parse4 r;
-	r.defer = !runt & (vlan | arp | (is4 & !s4 & !ihl5 & !ihlx) | (is6 & !s6 & (ext | t6far)));
-	const bool sip = (is4 & (s4 | ihlx)) | (is6 & s6);   // short IP header
+	r.defer = !runt & ((vlan & !vshort) | (ARPP & arp & !arpbad) | (is4 & !s4 & !ihl5 & !ihlx) |
+			   (is6 & !s6 & (ext | t6far)));
+	const bool sip = (is4 & (s4 | ihlx)) | (is6 & s6) | arpbad;   // IP / ARP header fails
 	const bool sl4 = (is4 & !s4 & ab4) | (is6 & !s6 & ab6);
 	r.abort_at = pick(runt, ST_ETH, pick(sip, ST_IP, pick(sl4, ST_L4, NST)));
 	const uint32_t l4 = pick(is4, pick(u4, 17u, pick(t4, 6u, 0u)), pick(is6, pick(u6, 17u, pick(t6, 6u, 0u)), 0u));
