@@ -1,8 +1,4 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_qt.py tests/test_gpu_scale.py tests/test_gpu.py > gpurun_out/pytest_s20.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_s20.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/pytest_s20.log | head -20; exit $rc; }
-SC="1000000:500:250"
-for r in 1 2 3; do
-for v in late early; do
-XFG_LIB=$PWD/tools/abl/$v.so timeout -k 10 300 python -u tools/explore.py --log2-packets 26 --rounds 3 --iters 5 $SC > gpurun_out/explore_${v}_s20_$r.log 2>&1 || exit 2
-sed "s/^/$v /" gpurun_out/explore_${v}_s20_$r.log | grep scenario
-done; done
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/pytest_s22.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_s22.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/pytest_s22.log | head -20; exit $rc; }
+timeout -k 10 600 python -u tools/bench_configs.py c4 c5 c3sd c2 > gpurun_out/configs_s22.log 2>&1 || { tail -20 gpurun_out/configs_s22.log; exit 1; }
+grep "^{" gpurun_out/configs_s22.log | cut -c1-330
