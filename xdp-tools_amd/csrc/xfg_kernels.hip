@@ -1279,9 +1279,14 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * S + tid] : 0u;
 	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
 		hist[i] = 0;
+#ifdef XFG_DIAG
+	const bool normw = (a.diag & 8192) != 0;   // (diagnostics: no counter read-modify-write)
+#else
+	constexpr bool normw = false;
+#endif
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++)
-		val[j] = gid[j] != CT_NONE ? *global_counter(a, gid[j]) : 0ull;
+		val[j] = gid[j] != CT_NONE && !normw ? *global_counter(a, gid[j]) : 0ull;
 	if (tid < S)
 		s_fill[tid] = min(fl, cap);
 	__syncthreads();
@@ -1323,7 +1328,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++) {
 		const uint32_t k = tid + j * LC_THREADS;
-		if (gid[j] != CT_NONE && hist[k])
+		if (gid[j] != CT_NONE && hist[k] && !normw)
 			*global_counter(a, gid[j]) = val[j] + hist[k];
 	}
 }
