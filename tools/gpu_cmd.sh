@@ -1,7 +1,7 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONUNBUFFERED=1
 SC="1000000:500:250"
-cd /tmp && export TMPDIR=/tmp
-for m in 0 8192; do
-XFG_LIB=$GRAFT_REPO_ROOT/tools/abl/rmw.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_rmw$m -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/explore.py --log2-packets 26 --rounds 2 --iters 5 $SC:XFG_DIAG_MASK=$m > /dev/null 2>&1 || exit 3
-f=$(find $GRAFT_REPO_ROOT/gpurun_out/prof_rmw$m -name "*kernel_stats.csv" | head -1); echo "mask $m"; cut -d, -f1-4 $f | grep -E "count"
-done
+for r in 1 2 3; do
+for v in nw8 nw4; do
+XFG_LIB=$PWD/tools/abl/$v.so timeout -k 10 300 python -u tools/explore.py --log2-packets 26 --rounds 3 --iters 5 $SC $SC:XFG_DIAG_MASK=16 > gpurun_out/explore_${v}_s29_$r.log 2>&1 || exit 2
+sed "s/^/$v /" gpurun_out/explore_${v}_s29_$r.log | grep scenario
+done; done
