@@ -190,3 +190,43 @@ def test_qt_not_taken_with_both_directions_live(G):
     rules.v4_vals[:10] = 1                          # a src rule: both directions live
     data, lens = X.gen_workload(52, 3, 1 << 15, 64, v4=v4, ports=ports)
     run_both(G, "xdpfilt_dny_all", rules, data, lens, 64, path=2)
+
+
+def test_qt_counts_folded_across_batches_and_writes(G):
+    """The count kernel adds to QT-order counts that the runtime folds into
+    the canonical counters before any read, write or re-index: two batches
+    with no readout between them, then deletes + inserts (each folds first,
+    through the index being replaced), a third batch, one readout."""
+    variant = "xdpfilt_dny_all"
+    rules, v4, ports = one_direction_rules(61, 20000, 2)
+    data, lens = X.gen_workload(62, 3, 1 << 16, 64, v4=v4, ports=ports)
+    f = make_filter(G, variant, qt_min_keys=1, ipv4_capacity=1 << 16)
+    f.load_rules(rules)
+    cur = rules.prepared().copy()
+    feat = X.VARIANT_FEATURES[variant]
+    for _ in range(2):
+        v = f.run(data, lens, stride=64)
+        assert f.last_path() == 5
+        ov, cur, _ = X.run_oracle(feat, data, lens, cur, stride=64)
+        np.testing.assert_array_equal(v, ov)
+    gone = cur.v4_keys[:500]
+    for k in gone:
+        f.delete(G.MAP_IPV4, bytes(k))
+    nk = X.rand_keys(163, 700, 4)
+    nk = nk[~np.isin(nk.view("<u4").reshape(-1), cur.v4_keys.view("<u4").reshape(-1))][:500]
+    f.update_batch(G.MAP_IPV4, nk, np.full(len(nk), 2, np.uint64))
+    nxt = X.RuleSet()
+    nxt.ports = cur.ports
+    nxt.v4_keys = np.concatenate([cur.v4_keys[500:], nk])
+    nxt.v4_vals = np.concatenate([cur.v4_vals[500:], np.full(len(nk), 2, np.uint64)])
+    cur = nxt.prepared()
+    data, lens = X.gen_workload(64, 3, 1 << 16, 64, v4=cur.v4_keys, ports=ports)
+    v = f.run(data, lens, stride=64)
+    assert f.last_path() == 5
+    ov, cur, _ = X.run_oracle(feat, data, lens, cur, stride=64)
+    np.testing.assert_array_equal(v, ov)
+    got = gpu_values(f, G, cur)
+    for fld in ("ports", "v4_vals"):
+        np.testing.assert_array_equal(getattr(got, fld), getattr(cur, fld), err_msg=fld)
+    assert (cur.v4_vals >> np.uint64(6)).sum() > 0
+    f.close()

@@ -38,6 +38,8 @@ int xfg_launch_compact(const uint8_t *verdicts, uint64_t n, uint32_t action, uin
 		       unsigned long long *count, unsigned long long *status, uint32_t *ticket,
 		       unsigned grid, void *stream);
 uint64_t xfg_compact_tiles(uint64_t n);
+int xfg_launch_qt_fold(unsigned long long *qt_hits, const uint32_t *trans,
+		       unsigned long long *hits, uint32_t n, void *stream);
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
 #define XFG_HOST_REG_MAX 16 /* registered host buffers per context */
@@ -80,7 +82,12 @@ struct xfg_dev {
 	uint32_t *qt_img, *qt_trans;
 	uint64_t qt_img_bytes, qt_trans_bytes;
 	uint32_t qt_gen, qt_bits, qt_seed, qt_live, qt_n;
-	int last_kind;                  /* kernel kind of the last launch (-1: none) */
+	/* the count kernel's QT-order hit counts (xfg_kargs.qt_hits) and
+	 * whether a launch may have added to them since the last fold */
+	unsigned long long *qt_hits;
+	uint64_t qt_hits_bytes;
+	int qt_pending;
+	int last_kind;                 /* kernel kind of the last launch (-1: none) */
 	/* host-resident classify (xfg_classify_host / xfg_classify_xsk_host),
 	 * under host_lock: a gather pool, two fixed-size staging slots of
 	 * HOST_CH packets x HOST_WIN bytes (header windows, or whole slots of
@@ -344,6 +351,7 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->port_tab);
 	hipFree(d->qt_img);
 	hipFree(d->qt_trans);
+	hipFree(d->qt_hits);
 	free(d->port_flags_h);
 	hipFree(d->cstatus);
 	for (int k = 0; k < 2; k++) {
@@ -586,6 +594,37 @@ static unsigned long long *hits_view(xfg_ctx *ctx, struct xfg_dev *d, int mi)
 	return ctx->reduced ? d->m[mi].red_hits : d->m[mi].hits;
 }
 
+/* Add @d's QT-order hit counts into its canonical IPv4 counters, through the
+ * index's current qt_trans (d->lock held): in stream order after every
+ * classify that counted into them. */
+static int qt_fold_locked(struct xfg_dev *d)
+{
+	if (!d->qt_pending)
+		return 0;
+	int err = hip_err(hipSetDevice(d->ordinal));
+	if (!err)
+		err = xfg_launch_qt_fold(d->qt_hits, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
+	if (!err)
+		err = hip_err(hipStreamSynchronize(d->stream));
+	if (!err)
+		d->qt_pending = 0;
+	return err;
+}
+
+/* Before the IPv4 map's counters are read, written or reduced (ctx->lock
+ * held): fold every device's QT-order counts. */
+static int qt_fold(xfg_ctx *ctx, int mi)
+{
+	int err = 0;
+	for (int i = 0; mi == 0 && i < ctx->ndev && !err; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		pthread_mutex_lock(&d->lock);
+		err = qt_fold_locked(d);
+		pthread_mutex_unlock(&d->lock);
+	}
+	return err;
+}
+
 /* Read the per-device values of @slot of hash map @mi (0..2). */
 static int slot_values(xfg_ctx *ctx, int mi, uint64_t slot, uint64_t *vals)
 {
@@ -594,6 +633,9 @@ static int slot_values(xfg_ctx *ctx, int mi, uint64_t slot, uint64_t *vals)
 		return 0;
 	}
 	const struct xfg_table *t = &ctx->t[mi];
+	int e0 = qt_fold(ctx, mi);
+	if (e0)
+		return e0;
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
 		uint8_t f;
@@ -649,6 +691,9 @@ static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals)
 		return 0;
 	}
 	const struct xfg_table *t = &ctx->t[mi];
+	int e0 = qt_fold(ctx, mi);
+	if (e0)
+		return e0;
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
 		uint8_t f = vals[i] & 63;
@@ -926,6 +971,8 @@ int64_t xfg_map_lookup_batch(xfg_ctx *ctx, int map, const void *keys, uint64_t n
 			err = -ENOMEM;
 			goto out;
 		}
+		if (t && (err = qt_fold(ctx, map - 1)))
+			goto out;
 		for (int i = 0; i < ctx->ndev && !err; i++) {
 			struct xfg_dev *d = &ctx->dev[i];
 			const void *fsrc = t ? (const void *)d->m[map - 1].buckets : (const void *)d->port_flags;
@@ -1012,6 +1059,8 @@ static int update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t 
 			err = -ENOMEM;
 			goto out;
 		}
+		if ((err = qt_fold(ctx, mi)))
+			goto out;
 		for (int i = 0; i < nd && !err; i++) {
 			struct xfg_dev *d = &ctx->dev[i];
 			if (!fresh) {
@@ -1170,7 +1219,8 @@ static int qt_refresh(xfg_ctx *ctx, struct xfg_dev *d, uint32_t live)
 		return 0;
 	const uint64_t ib = (1ull << ctx->qt.bits) * XFG_QT_BUCKET, tb = (uint64_t)ctx->qt.nslots * 4;
 	pthread_mutex_lock(&d->lock);
-	if (!(err = scratch(d, (void **)&d->qt_img, &d->qt_img_bytes, ib)) &&
+	if (!(err = qt_fold_locked(d)) &&   /* (through the index being replaced) */
+	    !(err = scratch(d, (void **)&d->qt_img, &d->qt_img_bytes, ib)) &&
 	    !(err = scratch(d, (void **)&d->qt_trans, &d->qt_trans_bytes, tb)) &&
 	    !(err = dev_write(d, d->qt_img, ctx->qt.img, ib)) &&
 	    !(err = dev_write(d, d->qt_trans, ctx->qt.trans, tb))) {
@@ -1338,6 +1388,15 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.qt_seed = d->qt_seed;
 		a.qt_live = d->qt_live;
 		a.qt_n = d->qt_n;
+		/* its QT-order counts (zeroed when (re)allocated; a resize only
+		 * follows a fold: qt_refresh) */
+		const uint64_t qb = (uint64_t)d->qt_n * 8, had = d->qt_hits_bytes;
+		if ((err = scratch(d, (void **)&d->qt_hits, &d->qt_hits_bytes, qb)))
+			goto out;
+		if (d->qt_hits_bytes != had &&
+		    (err = hip_err(hipMemsetAsync(d->qt_hits, 0, d->qt_hits_bytes, d->stream))))
+			goto out;
+		a.qt_hits = d->qt_hits;
 	}
 	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
 #ifdef XFG_DIAG
@@ -1416,6 +1475,8 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		    (err = hip_err(hipStreamWaitEvent(d->stream, d->ev_user, 0))))
 			goto out;
 	}
+	if (a.qt_hits && iters > 0)
+		d->qt_pending = 1;
 	for (int i = 0; i < iters && !err; i++)
 		err = xfg_launch_classify(ctx->prog_features, &a, (unsigned)grid, d->stream);
 	if (!err)
@@ -2179,6 +2240,11 @@ int xfg_comm_allreduce(xfg_ctx *ctx)
 		return -EINVAL;
 	struct xfg_dev *d = &ctx->dev[0];
 	HIPCHK(hipSetDevice(d->ordinal));
+	pthread_mutex_lock(&d->lock);
+	err = qt_fold_locked(d);   /* (the QT-order counts into the counters reduced) */
+	pthread_mutex_unlock(&d->lock);
+	if (err)
+		return err;
 	HIPCHK(hipStreamSynchronize(d->stream));
 	ctx->reduced = 0;
 	if (ncclGroupStart() != ncclSuccess)

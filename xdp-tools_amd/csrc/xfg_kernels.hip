@@ -1268,13 +1268,15 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	// the identity span: hash-map + port counters, or the QT slots
 	const uint32_t total = a.qt ? a.qt_n : a.gbase[3] + 65536u;
 	// counters of histogram entries tid + j * LC_THREADS: identity, value
+	// (the quotient index: the QT-order counts, 16 slots a line)
 	uint32_t gid[J];
 	unsigned long long val[J];
+	auto ctr = [&](uint32_t g) { return a.qt_hits ? a.qt_hits + g : global_counter(a, g); };
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++) {
 		const uint32_t k = tid + j * LC_THREADS;
 		const uint32_t g = ((k >> 4) << 12) | (p << 4) | (k & 15);
-		gid[j] = k < hist_n && g < total ? (a.qt ? a.qt_trans[g] : g) : CT_NONE;
+		gid[j] = k < hist_n && g < total ? (a.qt_hits ? g : a.qt ? a.qt_trans[g] : g) : CT_NONE;
 	}
 	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * S + tid] : 0u;
 	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
@@ -1286,7 +1288,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 #endif
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++)
-		val[j] = gid[j] != CT_NONE && !normw ? *global_counter(a, gid[j]) : 0ull;
+		val[j] = gid[j] != CT_NONE && !normw ? *ctr(gid[j]) : 0ull;
 	if (tid < S)
 		s_fill[tid] = min(fl, cap);
 	__syncthreads();
@@ -1329,7 +1331,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	for (uint32_t j = 0; j < J; j++) {
 		const uint32_t k = tid + j * LC_THREADS;
 		if (gid[j] != CT_NONE && hist[k] && !normw)
-			*global_counter(a, gid[j]) = val[j] + hist[k];
+			*ctr(gid[j]) = val[j] + hist[k];
 	}
 }
 
@@ -1547,6 +1549,33 @@ extern "C" int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sin
 	hipLaunchKernelGGL(xfg_stream_read_kernel, dim3(grid), dim3(256), 0,
 			   static_cast<hipStream_t>(stream), static_cast<const u32x4 *>(src),
 			   bytes / 16, static_cast<u32x4 *>(sink));
+	return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Fold the QT-order hit counts into the canonical IPv4 counters (qt_trans
+// is injective: each canonical counter has at most one QT slot, so a plain
+// read-modify-write) and zero them.  Runs at readout, not per batch.
+__global__ __launch_bounds__(256) void xfg_qt_fold_kernel(unsigned long long *__restrict__ qh,
+							  const uint32_t *__restrict__ trans,
+							  unsigned long long *__restrict__ hits, uint32_t n)
+{
+	for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < n; q += gridDim.x * 256u) {
+		const unsigned long long v = qh[q];
+		if (v) {
+			const uint32_t c = trans[q];
+			if (c != CT_NONE)
+				hits[c] += v;
+			qh[q] = 0;
+		}
+	}
+}
+
+extern "C" int xfg_launch_qt_fold(unsigned long long *qt_hits, const uint32_t *trans,
+				  unsigned long long *hits, uint32_t n, void *stream)
+{
+	const uint32_t grid = n ? (n + 255) / 256 < 2048u ? (n + 255) / 256 : 2048u : 1u;
+	hipLaunchKernelGGL(xfg_qt_fold_kernel, dim3(grid), dim3(256), 0,
+			   static_cast<hipStream_t>(stream), qt_hits, trans, hits, n);
 	return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

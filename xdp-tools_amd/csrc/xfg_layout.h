@@ -193,6 +193,11 @@ struct xfg_kargs {
 	 * mapped to canonical ones by qt_trans; qt_live = the one live mask */
 	const uint32_t *qt;
 	const uint32_t *qt_trans;
+	/* hit counts of the QT slots (qt_n, QT-slot order): the count kernel
+	 * adds there, the host folds them into the canonical counters through
+	 * qt_trans before any counter read, write or re-index (the per-CPU
+	 * counters of BPF are summed at readout the same way) */
+	unsigned long long *qt_hits;
 	uint32_t qt_bits;
 	uint32_t qt_seed;
 	uint32_t qt_base;
