@@ -8,6 +8,7 @@
   c5  xdpfilt_dny_all, 1514 B frames, 15M IPv4 + 1M IPv6 dst rules + 1024
       dst-port rules: device-resident, and end to end from host memory
       (header windows H2D, verdicts D2H, xfg_classify_host)
+  c3  C3 itself at SURVEY.md §8d's 2^24 batch (bench.py times 2^26)
   c3sd  C3 with every rule src|dst (`-m src,dst`): both IPv4 lookups live,
       so a packet probes two keys (the case C3's all-dst census skips)
 
@@ -31,8 +32,8 @@ def run(name, args):
     import numpy as np
     import xftools as X
     import xfgpu as G
-    kind = {"c2": 2, "c4": 4, "c5": 5, "c3sd": 3}[name]
-    n = 1 << (args.log2_packets or {"c2": 24, "c4": 23, "c5": 23, "c3sd": 24}[name])
+    kind = {"c2": 2, "c3": 3, "c4": 4, "c5": 5, "c3sd": 3}[name]
+    n = 1 << (args.log2_packets or {"c2": 24, "c3": 24, "c4": 23, "c5": 23, "c3sd": 24}[name])
     stride = 64 if kind in (2, 3) else 1536
     n4 = {2: 1000, 3: 1_000_000, 4: 1_000_000, 5: 15_000_000}[kind]
     flag = 3 if name == "c3sd" else 2

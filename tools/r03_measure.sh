@@ -22,6 +22,6 @@ KNAME=pipeq bash tools/pmc.sh c3q_$TAG "--log2-packets 26 1000000:500:250" "FETC
 python3 tools/pmc_summary.py --kernel log_count "$OUT"/pmc_c3q_${TAG}_* > "$OUT/pmc_c3lc_$TAG.json"
 head -c 600 "$OUT/pmc_c3q_$TAG.json"
 unset XFG_LIB
-timeout -k 10 600 python -u tools/bench_configs.py c2 c4 c5 c3sd > "$OUT/configs_$TAG.log" 2>&1 || { tail -20 "$OUT/configs_$TAG.log"; exit 4; }
+timeout -k 10 600 python -u tools/bench_configs.py c2 c3 c4 c5 c3sd > "$OUT/configs_$TAG.log" 2>&1 || { tail -20 "$OUT/configs_$TAG.log"; exit 4; }
 cut -c1-300 "$OUT/configs_$TAG.log"
 exit 0
