@@ -127,6 +127,10 @@ int xfg_last_path(const xfg_ctx *ctx, int dev);
  *   delete:  -ENOENT if absent; ports: -EINVAL (array maps cannot delete).
  *   get_next_key: key==NULL => first key; -ENOENT after the last one.
  * Key sizes: ports 4 (u32, < 65536), ipv4 4, ipv6 16, ethernet 6.
+ * A value read after a classify includes every hit of the classifies queued
+ * before it on that device (the quotient-index path keeps its counts per
+ * index slot on the device; the first IPv4-map read, write or all-reduce
+ * after it folds them in, one kernel on the device's stream).
  */
 int xfg_map_lookup(xfg_ctx *ctx, int map, const void *key, uint64_t *vals);
 int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals);
