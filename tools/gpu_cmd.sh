@@ -1,3 +1,6 @@
+# Partition chunk-size A/B (C3, 2^26). Build the libraries first, on the CPU:
+#   tools/abbuild.sh base -DXFG_AB_C3; tools/abbuild.sh c4k -DXFG_AB_C3 -DXFG_LOG_CHUNK=4096
+#   tools/abbuild.sh c16k -DXFG_AB_C3 -DXFG_LOG_CHUNK=16384
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONUNBUFFERED=1
 SC="1000000:500:250"
 for r in 1 2 3; do
