@@ -230,3 +230,114 @@ def test_qt_counts_folded_across_batches_and_writes(G):
         np.testing.assert_array_equal(getattr(got, fld), getattr(cur, fld), err_msg=fld)
     assert (cur.v4_vals >> np.uint64(6)).sum() > 0
     f.close()
+
+
+def crowd(seed, bits=QT_BITS, need=40):
+    """Random keys that all home in one index bucket (the fullest of 2^23)."""
+    rng = np.random.default_rng(seed)
+    cand = rng.integers(0, 2**32, 1 << 23, dtype=np.uint64).astype(np.uint32)
+    cu8 = cand.view(np.uint8).reshape(-1, 4)
+    b = qt_bucket(cu8, bits)
+    same = cu8[b == np.argmax(np.bincount(b))]
+    assert len(same) >= need
+    return same
+
+
+def test_qt_single_edits_between_batches(G):
+    """Single-rule edits (xfg_map_update / xfg_map_delete, one key each, as the
+    CLI makes them) patch the index in place between batches: a bucket filled
+    to 16, the 17th key that turns entry 15 into the overflow marker, deletes
+    that leave holes, inserts into those holes, flag changes that take keys
+    out of and back into the index, and single inserts / deletes spread over
+    the map -- each group followed by a batch aimed at the edited keys,
+    checked bit-exactly (verdicts, every rule value, stats) against the
+    restatement with the same edits.  Contract: map_set_flags / bpf_map_*_elem
+    edits between packets, xdp-filter/xdp-filter.c:111-157."""
+    variant = "xdpfilt_dny_all"
+    feat = X.VARIANT_FEATURES[variant]
+    rules, v4, ports = one_direction_rules(71, 20000, 2)
+    same = crowd(72)
+    rules.v4_keys = np.concatenate([same[:16], v4])      # one bucket exactly full
+    rules.v4_vals = np.concatenate([np.full(16, 2, np.uint64), rules.v4_vals])
+    f = make_filter(G, variant, qt_min_keys=1, ipv4_capacity=1 << 16)
+    f.load_rules(rules)
+    cur = {bytes(k): int(v) for k, v in zip(rules.v4_keys, rules.v4_vals)}
+    rng = np.random.default_rng(73)
+
+    def batch(seed, aim):
+        nonlocal cur
+        rs = X.RuleSet()
+        rs.ports = rules.ports
+        ks = list(cur)
+        rs.v4_keys = np.frombuffer(b"".join(ks), np.uint8).reshape(-1, 4).copy()
+        rs.v4_vals = np.array([cur[k] for k in ks], np.uint64)
+        data, lens = X.gen_workload(seed, 3, 1 << 15, 64, v4=rs.v4_keys, ports=ports)
+        d = data.reshape(-1, 64)
+        ip4 = np.nonzero((d[:, 12] == 8) & (d[:, 13] == 0) & (lens >= 62))[0][:6000]
+        aim = np.asarray(aim, np.uint8).reshape(-1, 4)
+        d[ip4, 30:34] = aim[np.arange(len(ip4)) % len(aim)]
+        v = f.run(data, lens, stride=64)
+        assert f.last_path() == 5
+        ov, orules, ost = X.run_oracle(feat, data, lens, rs, stride=64)
+        assert_same(v, gpu_values(f, G, rs), f.stats(), ov, orules, ost)
+        f.stats_reset()
+        cur = {bytes(k): int(x) for k, x in zip(orules.v4_keys, orules.v4_vals)}
+
+    batch(74, same[:24])
+    # the 17th key homed in the full bucket: entry 15 becomes the marker
+    for k in same[16:18]:
+        f.update(G.MAP_IPV4, bytes(k), 2)
+        cur[bytes(k)] = 2
+    batch(75, same[:24])
+    # holes: delete 3 of the bucket's keys (one of them maybe the spilled
+    # one), then insert 2 new keys homed there
+    for k in same[[1, 5, 16]]:
+        f.delete(G.MAP_IPV4, bytes(k))
+        del cur[bytes(k)]
+    batch(76, same[:24])
+    for k in same[18:20]:
+        f.update(G.MAP_IPV4, bytes(k), 2 | (3 << 6))
+        cur[bytes(k)] = 2 | (3 << 6)
+    batch(77, same[:24])
+    # flags: the live bit off for 40 keys, back on for 20 of them
+    ks = [bytes(k) for k in v4[rng.choice(len(v4), 40, replace=False)] if bytes(k) in cur]
+    for k in ks:
+        nv = (cur[k] & ~3) | 4
+        f.update(G.MAP_IPV4, k, nv)
+        cur[k] = nv
+    batch(78, np.frombuffer(b"".join(ks), np.uint8))
+    for k in ks[:20]:
+        nv = (cur[k] & ~7) | 2
+        f.update(G.MAP_IPV4, k, nv)
+        cur[k] = nv
+    batch(79, np.frombuffer(b"".join(ks), np.uint8))
+    # 50 single deletes and 50 single inserts over the map
+    gone = [bytes(k) for k in v4[rng.choice(len(v4), 50, replace=False)] if bytes(k) in cur]
+    for k in gone:
+        f.delete(G.MAP_IPV4, k)
+        del cur[k]
+    nk = X.rand_keys(80, 80, 4)
+    nk = [bytes(k) for k in nk if bytes(k) not in cur][:50]
+    for k in nk:
+        f.update(G.MAP_IPV4, k, 2)
+        cur[k] = 2
+    batch(81, np.frombuffer(b"".join(gone + nk), np.uint8))
+    f.close()
+
+
+def test_qt_falls_back_when_the_log_cannot_run(G):
+    """qt_min_keys=1 with maps small enough that every counter has a direct
+    LDS counter: the hit log (the index kernel's only counting path) is not
+    set up, so the launch takes the IPv4-key kernel -- a result, not -EIO
+    (launch_batch decides the kernel from the log's conditions)."""
+    rules, v4, ports = one_direction_rules(91, 300, 2)
+    data, lens = X.gen_workload(92, 3, 1 << 15, 64, v4=v4, ports=ports)
+    ov, orules, ost = X.run_oracle(X.VARIANT_FEATURES["xdpfilt_dny_all"], data, lens, rules,
+                                   stride=64)
+    f = make_filter(G, "xdpfilt_dny_all", qt_min_keys=1, ipv4_capacity=512,
+                    ipv6_capacity=16, eth_capacity=16)
+    f.load_rules(rules)
+    v = f.run(data, lens, stride=64)
+    assert f.last_path() == 2
+    assert_same(v, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
+    f.close()

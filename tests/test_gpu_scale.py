@@ -1,16 +1,19 @@
 """GPU parity at the bench's own batch size (SURVEY.md §8d's C3, as bench.py
-runs it): everything sized by the batch -- the hit-log partition
-sub-buffers (2 n / 2048 + 256 entries each, 8 per partition, spilling to
-atomics past that, xfg_ctx.c launch_batch), the per-wave deferred lists and hit-log regions,
-the count kernel -- is checked against the CPU restatement (oracle/) on
+runs it): everything sized by the batch -- the hit-log partition slices
+(one per partition and classify workgroup, 2 * ceil(wg_max / 256) + 64
+entries, wg_max = the most packets a workgroup's waves can log; a fuller
+slice spills to the canonical counters, xfg_ctx.c launch_batch), the
+per-wave deferred lists and hit-log regions, the count kernel -- is checked
+against the CPU restatement (oracle/) on
 every host thread, bit-exact: verdicts, all 1M rule values, per-action
 stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
 
   * C3 at 2^26 packets, 16-bit lengths: bench.py's rank-0 shard exactly;
   * a skewed C3 at 2^25: every hit on one of 8 hot rules, so each hot
-    rule's hits alone (~1.9M) overfill its hit-log partition's
-    sub-buffers (8 x ~33k entries): the spill-to-atomics path runs at
-    scale.
+    rule's hits in one workgroup (~1.9M over the grid) overfill that
+    workgroup's slice of the rule's partition several times over: the
+    spill path (log_counter: straight to the canonical counter, beside the
+    logged entries that reach the QT-order counters) runs at scale.
 """
 import os
 
@@ -80,8 +83,14 @@ def test_c3_skewed_hits_overfill_log_partitions_2p25(G):
     data, lens = X.gen_workload(33, 3, n, 64, v4=hot, ports=ports, dst_permille=500,
                                 port_permille=250, bad_permille=10)
     _, orules = _check(G, rules, data, lens.astype(np.uint16))
-    pcap = 8 * (2 * ((n + 2047) // 2048) + 256)   # a partition's 8 sub-buffers
     hits = orules.v4_vals[:8] >> 6
-    assert (hits > pcap).all(), (hits, pcap)   # each hot rule alone overfills a partition
+    # launch_batch's slice capacity for the QT kernel's grid (2 workgroups of
+    # 8 waves per CU, 256 CUs on MI355X; any grid of 128-1024 workgroups
+    # gives the same verdict): a hot rule's hits per workgroup exceed it
+    for grid in (128, 256, 512, 1024):
+        nw, nt = grid * 8, (n + 63) // 64
+        wg_max = 8 * ((nt + nw - 1) // nw * 64)
+        pcap = (2 * ((wg_max + 255) // 256) + 64 + 7) & ~7
+        assert (hits // grid > 2 * pcap).all(), (grid, hits, pcap)
     # (the other rules only see random addresses that happen to be ruled)
     assert int((orules.v4_vals[8:] >> 6).sum()) < n // 1000

@@ -11,6 +11,6 @@ P=xdp-tools_amd
   -Iinclude -I$P/csrc -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
   -c $P/csrc/xfg_kernels.hip -o tools/abl/$name.o
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/abl/$name.so \
-  $P/build/xfg_ctx_diag.o $P/build/xfg_table.o $P/build/xfg_io.o tools/abl/$name.o \
+  $P/build/xfg_ctx_diag.o $P/build/xfg_table_diag.o $P/build/xfg_io.o tools/abl/$name.o \
   -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread -Wl,-rpath,/opt/rocm/lib
 rm -f tools/abl/$name.o

@@ -668,30 +668,86 @@ static uint32_t census_mask(const uint32_t *cnt)
 }
 
 /* @any / @all: the OR / AND over devices of the slot's flag byte (bit 7 of
- * the census byte records that they differ) */
-static void flags_note(xfg_ctx *ctx, int mi, uint64_t slot, uint8_t any, uint8_t all)
+ * the census byte records that they differ).  A changed IPv4 flag byte
+ * marks the quotient index for a rebuild unless @patch (a single edit, which
+ * slot_store applies to the index in place); returns the old byte. */
+static uint8_t flags_note(xfg_ctx *ctx, int mi, uint64_t slot, uint8_t any, uint8_t all, int patch)
 {
-	const uint8_t f = any | (any != all ? 0x80 : 0);
-	census(ctx->flag_cnt[mi], ctx->flag_or[mi][slot], f);
+	const uint8_t f = any | (any != all ? 0x80 : 0), old = ctx->flag_or[mi][slot];
+	census(ctx->flag_cnt[mi], old, f);
 	ctx->flag_or[mi][slot] = f;
-	if (mi == 0)
+	if (mi == 0 && old != f && !patch)
 		ctx->qt_dirty = 1;
+	return old;
 }
 
-static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals)
+/* One IPv4 key's flag byte went from @old to @nw (ctx->lock held, every
+ * device's QT-order counts folded): enter it into or take it out of the
+ * quotient index in place (xfg_qt_patch) and send the one bucket and its
+ * trans[] entries to every device whose copy was current; a change of the
+ * index's size (bits follow the key count) leaves a full rebuild to the
+ * next classify, as before.  @key: the key bytes (NULL: read from the
+ * table, where the key still is). */
+static int qt_edit(xfg_ctx *ctx, uint64_t slot, const void *key, uint8_t old, uint8_t nw)
+{
+	struct xfg_qt *q = &ctx->qt;
+	if (ctx->qt_dirty || !ctx->qt_gen || !q->img)
+		return 0;   /* (rebuilt before its next use anyway) */
+	const int was = (old & q->live) == q->live, is = (nw & q->live) == q->live;
+	if (was == is)
+		return 0;
+	if (xfg_qt_bits_for(ctx->t[0].count) != q->bits) {
+		ctx->qt_dirty = 1;
+		return 0;
+	}
+	uint32_t k;
+	if (key)
+		memcpy(&k, key, 4);
+	else if (xfg_table_slot_key(&ctx->t[0], slot, &k)) {
+		ctx->qt_dirty = 1;
+		return 0;
+	}
+	const uint32_t b = xfg_qt_patch(q, k, (uint32_t)slot, is);
+	uint32_t gen = ctx->qt_gen + 1;
+	if (!gen)
+		gen = 1;
+	int err = 0;
+	for (int i = 0; i < ctx->ndev; i++) {
+		struct xfg_dev *d = &ctx->dev[i];
+		pthread_mutex_lock(&d->lock);
+		if (d->qt_gen == ctx->qt_gen) {
+			int e = dev_write(d, (uint8_t *)d->qt_img + (uint64_t)b * XFG_QT_BUCKET,
+					  q->img + (uint64_t)b * XFG_QT_SLOTS, XFG_QT_BUCKET);
+			if (!e)
+				e = dev_write(d, d->qt_trans + (uint64_t)b * XFG_QT_SLOTS,
+					      q->trans + (uint64_t)b * XFG_QT_SLOTS, XFG_QT_SLOTS * 4);
+			if (!e)
+				d->qt_gen = gen;
+			else if (!err)
+				err = e;
+		}
+		pthread_mutex_unlock(&d->lock);
+	}
+	ctx->qt_gen = gen;
+	return err;
+}
+
+static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals, const void *key)
 {
 	uint8_t any = 0, all = 63;
 	for (int i = 0; i < (ctx->ndev ? ctx->ndev : 1); i++) {
 		any |= vals[i] & 63;
 		all &= vals[i] & 63;
 	}
-	flags_note(ctx, mi, slot, any, all);
+	const uint8_t old = flags_note(ctx, mi, slot, any, all, ctx->ndev != 0);
 	if (!ctx->ndev) {
 		ctx->host_vals[mi][slot] = vals[0];
 		return 0;
 	}
 	const struct xfg_table *t = &ctx->t[mi];
 	int e0 = qt_fold(ctx, mi);
+	if (!e0 && mi == 0 && old != ctx->flag_or[0][slot])
+		e0 = qt_edit(ctx, slot, key, old, ctx->flag_or[0][slot]);
 	if (e0)
 		return e0;
 	for (int i = 0; i < ctx->ndev; i++) {
@@ -863,7 +919,7 @@ int xfg_map_update(xfg_ctx *ctx, int map, const void *key, const uint64_t *vals)
 		if (err)
 			goto out;
 	}
-	err = slot_store(ctx, mi, (uint64_t)s, vals);
+	err = slot_store(ctx, mi, (uint64_t)s, vals, key);
 out:
 	pthread_mutex_unlock(&ctx->lock);
 	return err;
@@ -891,7 +947,7 @@ int xfg_map_delete(xfg_ctx *ctx, int map, const void *key)
 			err = -ENOMEM;
 			goto out;
 		}
-		err = slot_store(ctx, mi, (uint64_t)s, z);
+		err = slot_store(ctx, mi, (uint64_t)s, z, key);
 		if (z != zero)
 			free(z);
 	}
@@ -1089,7 +1145,7 @@ static int update_batch(xfg_ctx *ctx, int map, const void *keys, const uint64_t 
 			any |= VAL(i, d) & 63;
 			all &= VAL(i, d) & 63;
 		}
-		flags_note(ctx, mi, (uint64_t)s, any, all);
+		flags_note(ctx, mi, (uint64_t)s, any, all, 0);
 		if (nd) {
 			for (int d = 0; d < nd; d++) {
 				img[ib * d + xfg_table_flag_off(t, s)] = VAL(i, d) & 63;
@@ -1368,7 +1424,6 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	if (cm && !strcmp(cm, "atomic"))
 		a.qt = NULL;             /* (the QT kernel counts through the hit log only) */
 #endif
-	const int kind = a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
 	/* small rule sets: a direct LDS counter per hash-map slot (their few
 	 * counters are hot: more than the LDS counter cache holds) */
 	if (a.gbase[3] <= XFG_DCNT_MAX)
@@ -1381,6 +1436,25 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * d->lock for that): its kind and its longest displacement */
 	a.port_tab = d->port_tab_ok ? d->port_tab : NULL;
 	a.port_tab_disp = d->port_tab_disp;
+	/* the hit log (below) decides whether the quotient-index kernel can run:
+	 * it counts through the log only.  Where the log cannot be set up (every
+	 * counter has a direct LDS counter, or the grid has more workgroups than
+	 * the log has slices) the IPv4-key kernel takes the batch instead. */
+	const int logged = a.t4.count || a.t6.count || a.te.count;
+	const int log_off = !a.pipe || !logged || a.dcnt >= a.gbase[3] || (cm && !strcmp(cm, "atomic"));
+	if (a.qt) {
+		const int k5 = 5, wi5 = a.window > 64;
+		const int pc = d->occ[k5][wi5][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
+		const uint64_t pw = (uint64_t)xfg_classify_threads(k5, a.window);
+		uint64_t g5 = (uint64_t)d->ncu * (pc > 0 ? pc : 1), need5 = (a.n + pw - 1) / pw;
+		if (g5 > need5)
+			g5 = need5 ? need5 : 1;
+		const uint64_t span = (uint64_t)d->qt_n;
+		const uint64_t hist5 = ((span + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
+		if (log_off || g5 > XFG_LOG_SLICES_MAX || hist5 > XFG_LOG_HIST_MAX)
+			a.qt = NULL;
+	}
+	const int kind = a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
 	if (a.qt) {   /* the index in stream order at this launch */
 		a.qt = d->qt_img;
 		a.qt_trans = d->qt_trans;
@@ -1444,10 +1518,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	/* (with the quotient index the log holds QT slots only: its span) */
 	uint64_t total = a.qt ? (uint64_t)a.qt_n : (uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES;
 	uint64_t hist = ((total + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
-	int logged = a.t4.count || a.t6.count || a.te.count;
-	if (a.pipe && logged && a.dcnt < a.gbase[3] && hist <= XFG_LOG_HIST_MAX &&
-	    grid <= XFG_LOG_SLICES_MAX &&
-	    !(cm && !strcmp(cm, "atomic"))) {
+	if (!log_off && hist <= XFG_LOG_HIST_MAX && grid <= XFG_LOG_SLICES_MAX) {
 		/* slice (partition, workgroup): twice a uniform share of the
 		 * most the workgroup's waves can log (a fuller one spills) */
 		uint64_t wg_max = (per_wg / 64) * (uint64_t)a.defer_cap;
@@ -1466,7 +1537,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.pslices = (uint32_t)grid;
 		a.log_hist = (uint32_t)hist;
 	}
-	if (a.qt && !a.tlog) {   /* (fill_kargs checked that the log covers the index) */
+	if (a.qt && !a.tlog) {   /* (decided above: cannot happen) */
 		err = -EIO;
 		goto out;
 	}

@@ -837,17 +837,20 @@ struct Counters {
 // The pipelined kernels' counting of hash-map hits (kargs.tlog != NULL):
 //   1. each wave appends its hits' counter identities to its own region,
 //      one coalesced store per tile (log_append);
-//   2. at its end each workgroup sorts its entries by partition
+//   2. at its end each workgroup counting-sorts its entries by partition
 //      (g >> 4) % XFG_LOG_PARTS -- 16 consecutive counters, one 128-byte
-//      line of u64, per chunk; chunks dealt round-robin -- reserving its
-//      slice of every partition's buffer with one atomic per partition
-//      (log_partition);
-//   3. xfg_log_count_kernel, one workgroup per partition, sums the
-//      partition in an LDS histogram and adds each count to its counter
-//      with a plain read-modify-write (it owns those counters).
+//      line of u64, per chunk; chunks dealt round-robin -- and writes them,
+//      as 16-bit indices local to the partition (log_local), into its OWN
+//      slice of every partition's buffer: slice (partition p, workgroup b)
+//      at pbuf[(p * pslices + b) * pcap], its fill written (not reserved,
+//      no atomics) to pfill[p * pslices + b] (log_partition);
+//   3. xfg_log_count_kernel, one workgroup per partition, reads the
+//      partition's slices one after another into an LDS histogram and adds
+//      each count to its counter with a plain read-modify-write (it owns
+//      those counters).
 // Every hit costs a 4-byte coalesced store and two L2-resident passes
-// instead of a random memory-side atomic.  A partition buffer that would
-// overflow sends the excess to atomics (exact either way).
+// instead of a random memory-side atomic.  Entries past a slice's pcap go
+// straight to their counter with an atomic (log_counter; exact either way).
 __device__ __forceinline__ uint32_t log_part(uint32_t g) { return (g >> 4) & (XFG_LOG_PARTS - 1); }
 __device__ __forceinline__ uint32_t log_local(uint32_t g) { return ((g >> 12) << 4) | (g & 15); }
 

@@ -11,9 +11,11 @@
 static uint32_t buckets_for(uint32_t capacity, uint32_t spb)
 {
 	double lf = spb >= 12 ? 0.6 : (spb >= 6 ? 0.55 : 0.45);
-	const char *e = spb >= 12 ? getenv("XFG_LF4") : NULL;   /* diagnostics only */
+#ifdef XFG_DIAG
+	const char *e = spb >= 12 ? getenv("XFG_LF4") : NULL;   /* diagnostics build only */
 	if (e && atof(e) > 0.1 && atof(e) < 0.95)
 		lf = atof(e);
+#endif
 	uint64_t nb = (uint64_t)((double)capacity / (spb * lf)) + 1;
 	if (nb > 0x7fffffffull / spb - 1)
 		nb = 0x7fffffffull / spb - 1;
@@ -316,4 +318,42 @@ int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *fla
 	}
 	free(homed);
 	return 0;
+}
+
+uint32_t xfg_qt_patch(struct xfg_qt *q, uint32_t key, uint32_t slot, int add)
+{
+	const uint32_t rbits = 32 - q->bits, rmask = (1u << rbits) - 1;
+	const uint32_t h = xfg_qt_hash(key, q->seed), b = h >> rbits;
+	const uint16_t r = (uint16_t)(XFG_QT_USED | (h & rmask));
+	uint16_t *e = q->img + (uint64_t)b * XFG_QT_SLOTS;
+	uint32_t *tr = q->trans + (uint64_t)b * XFG_QT_SLOTS;
+	if (!add) {
+		for (uint32_t c = 0; c < XFG_QT_SLOTS; c++)
+			if (e[c] == r) {   /* (keys are unique: at most one entry) */
+				e[c] = 0;
+				tr[c] = 0xffffffffu;
+				q->placed--;
+				return b;
+			}
+		if (q->spilled)
+			q->spilled--;
+		return b;
+	}
+	const int marked = e[XFG_QT_SLOTS - 1] == XFG_QT_OVF_MARK;
+	const uint32_t room = marked ? XFG_QT_SLOTS - 1 : XFG_QT_SLOTS;
+	for (uint32_t c = 0; c < room; c++)
+		if (!(e[c] & XFG_QT_USED)) {
+			e[c] = r;
+			tr[c] = slot;
+			q->placed++;
+			return b;
+		}
+	if (!marked) {   /* entry 15's key and this one go to the canonical table */
+		e[XFG_QT_SLOTS - 1] = XFG_QT_OVF_MARK;
+		tr[XFG_QT_SLOTS - 1] = 0xffffffffu;
+		q->placed--;
+		q->spilled++;
+	}
+	q->spilled++;
+	return b;
 }

@@ -90,6 +90,16 @@ struct xfg_qt {
 };
 int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *flags,
 		 uint32_t live, uint32_t seed);
+/* One key entering (@add) or leaving the index in place, for a single map
+ * edit between rebuilds: @key at canonical @slot.  An entry goes into the
+ * first free entry of its bucket; a full bucket without the overflow marker
+ * gives up its entry 15 to the marker (that key and the new one are then
+ * answered by the canonical table); a leaving key's entry is cleared (a
+ * spilled one leaves nothing to clear).  The marker is never cleared here:
+ * a marked bucket only sends its misses to the canonical table, which is
+ * always exact.  Returns the bucket touched.  The caller has folded the
+ * QT-order counts first: an entry given to another key must count from 0. */
+uint32_t xfg_qt_patch(struct xfg_qt *q, uint32_t key, uint32_t slot, int add);
 void xfg_qt_free(struct xfg_qt *q);
 /* Bucket bits for @count keys: fewer than XFG_QT_LOAD keys per 16-entry
  * bucket on average (a 1M-key map: 2^17 buckets, 4 MB). */
