@@ -4,6 +4,8 @@ capacities, strides and frame mixes the bench and DESIGN.md quote.
 Bit-exact: verdicts, every rule's value (hits << 6 | flags) and the
 per-action stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
 
+  C1  xdpfilt_alw_eth, the 8 MAC rules 02:00:00:00:00:0{1..8} (4 dst, 4
+      src), 64 B frames, 25% carrying a ruled MAC, 2^22 packets
   C2  xdpfilt_dny_ip, 1,000 IPv4 dst rules, ipv4_capacity=1000 (the direct
       LDS counter path, kargs.dcnt), 64 B dense frames, 2^22 packets
   C3  xdpfilt_dny_all, 1M IPv4 dst rules at capacity 1M + 16 dst-port rules,
@@ -62,6 +64,16 @@ def check(G, variant, rules, data, lens, stride, host=False, **caps):
         assert_same(vh, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
         f.close()
     return ov
+
+
+@pytest.mark.timeout(300)
+def test_c1_alw_eth_8_mac_rules(G):
+    rules = X.c1_rules()
+    data, lens = X.gen_c1(1, 1 << 22)
+    ov = check(G, "xdpfilt_alw_eth", rules, data, lens, 64)
+    # a quarter of the frames carry a ruled MAC where its rule tests it: DROP
+    # under allow mode (xdpfilt_prog.h:187-196)
+    assert abs(int((ov == 1).sum()) - (1 << 20)) < (1 << 14)
 
 
 @pytest.mark.timeout(300)

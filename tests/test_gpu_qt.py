@@ -262,12 +262,13 @@ def test_qt_single_edits_between_batches(G):
     f = make_filter(G, variant, qt_min_keys=1, ipv4_capacity=1 << 16)
     f.load_rules(rules)
     cur = {bytes(k): int(v) for k, v in zip(rules.v4_keys, rules.v4_vals)}
+    cur_ports = rules.ports.copy()
     rng = np.random.default_rng(73)
 
     def batch(seed, aim):
-        nonlocal cur
+        nonlocal cur, cur_ports
         rs = X.RuleSet()
-        rs.ports = rules.ports
+        rs.ports = cur_ports
         ks = list(cur)
         rs.v4_keys = np.frombuffer(b"".join(ks), np.uint8).reshape(-1, 4).copy()
         rs.v4_vals = np.array([cur[k] for k in ks], np.uint64)
@@ -282,6 +283,7 @@ def test_qt_single_edits_between_batches(G):
         assert_same(v, gpu_values(f, G, rs), f.stats(), ov, orules, ost)
         f.stats_reset()
         cur = {bytes(k): int(x) for k, x in zip(orules.v4_keys, orules.v4_vals)}
+        cur_ports = orules.ports.copy()
 
     batch(74, same[:24])
     # the 17th key homed in the full bucket: entry 15 becomes the marker

@@ -12,6 +12,13 @@
   c3sd  C3 with every rule src|dst (`-m src,dst`): both IPv4 lookups live,
       so a packet probes two keys (the case C3's all-dst census skips)
 
+  c1  xdpfilt_alw_eth, the 8 MAC rules 02:00:00:00:00:0{1..8} (4 dst, 4
+      src), 64 B Ethernet/IPv4/UDP frames, 25% carrying a ruled MAC (SURVEY.md
+      §8d: BASELINE.json configs[0], the reference's in-kernel CPU case): the
+      GPU path, and the CPU restatement timed on the same batch on 1 thread
+      and on every usable host core (SURVEY §8d CPU item 2; the in-kernel
+      veth run itself needs a BPF toolchain this image lacks)
+
 Roofline bytes per packet are min(len, 128) + 1.
 Usage: python3 tools/bench_configs.py [c2] [c4] [c5] [--log2-packets N]
 """
@@ -28,10 +35,65 @@ sys.path.insert(0, os.path.join(ROOT, "xdp-tools_amd", "python"))
 HBM_PEAK_GBS = 8000.0
 
 
+def run_c1(args):
+    import numpy as np
+    import xftools as X
+    import xfgpu as G
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 1 << (args.log2_packets or 24)
+    rules = X.c1_rules()
+    data, lens = X.gen_c1(1, n)
+    f = G.Filter(X.VARIANT_FEATURES["xdpfilt_alw_eth"], devices=[0])
+    assert f.prog_name == "xdpfilt_alw_eth"
+    f.load_rules(rules)
+    alg = int(np.minimum(lens.astype(np.int64), 128).sum() + n)
+    d_data, d_lens, d_verd = f.alloc(data.nbytes), f.alloc(lens.nbytes), f.alloc(n)
+    d_data.upload(data)
+    d_lens.upload(lens)
+    f.classify_timed(d_data.ptr, d_lens.ptr, n, 64, d_verd.ptr, 2)
+    ms = f.classify_timed(d_data.ptr, d_lens.ptr, n, 64, d_verd.ptr, args.iters)
+    path = f.last_path()
+    f.close()
+    # the CPU restatement on the same batch: 1 thread and every usable core
+    # (a bounded sample: whole passes until ~4 s each)
+    feats = X.VARIANT_FEATURES["xdpfilt_alw_eth"]
+    m = min(n, 1 << 22)
+    prepared = rules.prepared()
+    maps = X.OracleMaps(prepared, hashed=True)
+
+    def rate(threads, secs=4.0):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            X.run_oracle(feats, data[:m * 64], lens[:m], prepared, stride=64, maps=maps,
+                         nthreads=threads)
+            done += m
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return done / el / 1e6
+    nt = bench.host_threads()
+    r1, rn = rate(1), rate(nt)
+    line = {"config": "c1", "program": "xdpfilt_alw_eth", "packets": n, "stride": 64,
+            "rules_eth": 8, "kernel_path": path, "kernel_ms": round(ms, 4),
+            "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+            "roofline": {"alg_bytes_per_launch": alg,
+                         "achieved_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "cpu_restatement": {"Mpps_1thread": round(r1, 2), "Mpps_all": round(rn, 2),
+                                "threads": nt, "cpu_model": bench.cpu_model(),
+                                "sample": f"2^{m.bit_length() - 1} packets of the same batch, "
+                                          "whole passes for ~4 s each"},
+            "in_kernel_xdp": "not measured: needs a BPF-capable clang, libbpf, bpffs, "
+                             "iproute2 and root, absent from this image"}
+    print(json.dumps(line), flush=True)
+
+
 def run(name, args):
     import numpy as np
     import xftools as X
     import xfgpu as G
+    if name == "c1":
+        return run_c1(args)
     kind = {"c2": 2, "c3": 3, "c4": 4, "c5": 5, "c3sd": 3}[name]
     n = 1 << (args.log2_packets or {"c2": 24, "c3": 24, "c4": 23, "c5": 23, "c3sd": 24}[name])
     stride = 64 if kind in (2, 3) else 1536

@@ -7,6 +7,12 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"; mkdir -p "$OUT"
 TAG=${TAG:-ab}
 export PYTHONUNBUFFERED=1
+if [ -n "$TESTS" ]; then
+  timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $TESTS \
+    > "$OUT/pytest_$TAG.log" 2>&1
+  rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|error" "$OUT/pytest_$TAG.log" | tail -3
+  [ $rc -eq 0 ] || { grep -E "^E |Error|FAILED" "$OUT/pytest_$TAG.log" | head -30; exit $rc; }
+fi
 if [ -n "$BENCH" ]; then
   timeout -k 10 400 python -u bench.py $BENCH > "$OUT/bench_$TAG.log" 2>&1
   rc=$?; echo "bench rc=$rc"; tail -c 2500 "$OUT/bench_$TAG.log"; echo

@@ -149,7 +149,23 @@ static uint32_t gen_bad(struct rng *r, const struct pools *pl, uint8_t *p, uint3
 	}
 }
 
-/* Workload generator.  kind: 2 = C2, 3 = C3, 4 = C4 (IMIX), 5 = C5 (1514).
+/* C1 (BASELINE.json configs[0]): a 64 B Ethernet/IPv4/UDP
+ * frame whose MACs are random except that with probability @hit_permille
+ * one ruled MAC is placed where its rule tests it: rule i of the 8 in the
+ * destination MAC for i < 4 (the dst rules), in the source MAC for i >= 4
+ * (the src rules).  @macs: the 8 ruled MACs, 6 bytes each. */
+static void gen_c1(struct rng *r, const struct pools *pl, uint8_t *p, uint32_t hit_permille)
+{
+	gen_good(r, pl, p, 0, 64, 0, 0);
+	if (pl->nm && rchance(r, hit_permille)) {
+		const uint32_t i = rbelow(r, pl->nm);
+		memcpy(p + (i < pl->nm / 2 ? 0 : 6), pl->mac + 6ull * i, 6);
+	}
+}
+
+/* Workload generator.  kind: 1 = C1 (MAC pool in @v6 as 6-byte keys, @n6 of
+ * them; dst_permille = the ruled-MAC fraction), 2 = C2, 3 = C3, 4 = C4 (IMIX),
+ * 5 = C5 (1514).
  * Frames are written at data + i*stride (stride >= the largest frame).
  * dst_permille: fraction (x1000) of IPv4/IPv6 dst addresses drawn from the
  * rule pools.  Returns 0, or -1 if stride is too small. */
@@ -160,6 +176,12 @@ int xfs_gen_workload(uint64_t seed, int kind, uint64_t n, uint32_t stride,
 		     uint32_t port_permille, uint32_t bad_permille)
 {
 	struct pools pl = { v4, n4, v6, n6, NULL, 0, ports, np };
+	if (kind == 1) {   /* C1: the MAC pool rides in the v6 arguments */
+		pl.mac = v6;
+		pl.nm = n6;
+		pl.v6 = NULL;
+		pl.n6 = 0;
+	}
 	static const uint32_t imix[12] = { 64, 64, 64, 64, 64, 64, 64, 570, 570, 570, 570, 1514 };
 	uint32_t need = kind == 4 || kind == 5 ? 1514 : 64;
 	if (stride < need)
@@ -175,7 +197,7 @@ int xfs_gen_workload(uint64_t seed, int kind, uint64_t n, uint32_t stride,
 			len = 1514;
 		else
 			len = 64;
-		if (kind == 2) {
+		if (kind == 1 || kind == 2) {
 			cls = 0;
 		} else {
 			uint32_t c = rbelow(&r, 10);
@@ -184,6 +206,13 @@ int xfs_gen_workload(uint64_t seed, int kind, uint64_t n, uint32_t stride,
 		if (bad_permille && rchance(&r, bad_permille)) {
 			memset(p, 0, need < stride ? need : stride);
 			lens[i] = gen_bad(&r, &pl, p, len);
+			continue;
+		}
+		if (kind == 1) {
+			gen_c1(&r, &pl, p, dst_permille);
+			for (uint32_t o = 42; o < len; o++)
+				p[o] = (uint8_t)(o * 7 + i);
+			lens[i] = len;
 			continue;
 		}
 		if (cls == 2 && len == 64)

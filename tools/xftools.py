@@ -138,6 +138,26 @@ def gen_workload(seed, kind, n, stride, v4=None, v6=None, ports=None,
     return data, lens
 
 
+C1_MACS = np.array([[2, 0, 0, 0, 0, i] for i in range(1, 9)], np.uint8)   # 02:00:00:00:00:0{1..8}
+
+
+def c1_rules():
+    """C1's rule set: the 8 MACs 02:00:00:00:00:0{1..8}, the
+    first 4 dst rules, the last 4 src rules (`xdp-filter ether -m dst|src`)."""
+    rules = RuleSet()
+    rules.eth_keys = C1_MACS.copy()
+    rules.eth_vals = np.array([2] * 4 + [1] * 4, np.uint64)
+    return rules
+
+
+def gen_c1(seed, n, stride=64, hit_permille=250, bad_permille=10, data=None, lens=None):
+    """C1's traffic: 64 B Ethernet/IPv4/UDP frames with random MACs, a ruled
+    MAC (where its rule tests it) in `hit_permille` of them, and the
+    Appendix A malformed classes in `bad_permille`."""
+    return gen_workload(seed, 1, n, stride, v6=C1_MACS, dst_permille=hit_permille,
+                        port_permille=0, bad_permille=bad_permille, data=data, lens=lens)
+
+
 def gen_fuzz(seed, n, stride=160, rules: RuleSet | None = None, port_pool=None):
     data = np.zeros(n * stride, np.uint8)
     lens = np.zeros(n, np.uint32)

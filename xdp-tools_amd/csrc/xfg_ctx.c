@@ -1440,7 +1440,11 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * it counts through the log only.  Where the log cannot be set up (every
 	 * counter has a direct LDS counter, or the grid has more workgroups than
 	 * the log has slices) the IPv4-key kernel takes the batch instead. */
-	const int logged = a.t4.count || a.t6.count || a.te.count;
+	/* (a few keys in all -- C1's 8 MAC rules -- are hot: the LDS counter
+	 * cache holds every one of them, where the log would send their hits
+	 * through a handful of overfull partitions to contended atomics) */
+	const uint64_t nkeys = (uint64_t)a.t4.count + a.t6.count + a.te.count;
+	const int logged = nkeys > XFG_LOG_MIN_KEYS;
 	const int log_off = !a.pipe || !logged || a.dcnt >= a.gbase[3] || (cm && !strcmp(cm, "atomic"));
 	if (a.qt) {
 		const int k5 = 5, wi5 = a.window > 64;

@@ -713,27 +713,32 @@ __device__ __forceinline__ uint32_t lookups(const xfg_kargs &a, const KS &ks, co
 	return MISS;
 }
 
-// Per-workgroup counter cache in LDS: direct-mapped on the counter identity.
-// A rule hit by many packets (a hot port, an attacked address) is summed
-// here and reaches memory once per workgroup; a slot already owned by a
-// different counter sends the bump straight to its global atomic.
-constexpr int CC_ENTRIES = 512;
+// Per-workgroup counter cache in LDS: open addressing on the counter
+// identity, CC_PROBES slots from its home.  A rule hit by many packets (a
+// hot port, an attacked address, one of a handful of MAC rules) is summed
+// here and reaches memory once per workgroup; when its probe run is owned by
+// other counters the bump goes straight to its global atomic.
+constexpr int CC_ENTRIES = 512, CC_PROBES = 4;
 
 // Returns true when the LDS cache absorbed the n bumps of counter `tag`.
 __device__ __forceinline__ bool cache_hit(uint32_t *s_ctag, uint32_t *s_ccnt, uint32_t tag,
 					  uint32_t n)
 {
-	const uint32_t e = (tag * 0x9E3779B1u) >> 23;   // 9 bits
-	uint32_t t = s_ctag[e];
-	if (t == CT_NONE) {
-		t = atomicCAS(&s_ctag[e], CT_NONE, tag);
-		if (t == CT_NONE)
-			t = tag;
+	uint32_t e = (tag * 0x9E3779B1u) >> 23;   // 9 bits
+	for (int q = 0; q < CC_PROBES; q++) {
+		uint32_t t = s_ctag[e];
+		if (t == CT_NONE) {
+			t = atomicCAS(&s_ctag[e], CT_NONE, tag);
+			if (t == CT_NONE)
+				t = tag;
+		}
+		if (t == tag) {
+			atomicAdd(&s_ccnt[e], n);
+			return true;
+		}
+		e = (e + 1) & (CC_ENTRIES - 1);
 	}
-	if (t != tag)
-		return false;
-	atomicAdd(&s_ccnt[e], n);
-	return true;
+	return false;
 }
 
 

@@ -96,6 +96,7 @@
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
 #define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
 #define XFG_LOG_SLICES_MAX 1024u  /* slices per partition: classify workgroups */
+#define XFG_LOG_MIN_KEYS  256u    /* fewer hash-map keys: LDS counter cache, no log */
 
 
 /* Per-hash-map descriptor passed to the kernel by value. */

@@ -40,6 +40,17 @@
 #ifndef XFG_QT_EARLY_L
 #define XFG_QT_EARLY_L 1
 #endif
+// (A/B: bucket loads as global loads (0) or buffer loads with aux XFG_QT_BKAUX;
+// window loads non-temporal (1) or plain (0))
+#ifndef XFG_QT_BKPOL
+#define XFG_QT_BKPOL 0
+#endif
+#ifndef XFG_QT_BKAUX
+#define XFG_QT_BKAUX 0
+#endif
+#ifndef XFG_QT_WIN_NT
+#define XFG_QT_WIN_NT 1
+#endif
 
 namespace {
 
@@ -65,8 +76,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 
 #ifdef XFG_DIAG
 	// (diagnostics: 1 no counting, 2 no bucket loads, 8 no verdict stores,
-	// 16 no workgroup-end partition, 2048 no deferred packets, 4096 hits as
-	// memory-side atomics into scratch instead of the hit log -- results wrong)
+	// 16 no workgroup-end partition, 32 no LDS row staging, 64 no parse, 128
+	// no stats or deferral lists, 2048 no deferred packets, 4096 hits as
+	// memory-side atomics into scratch instead of the hit log, 8192 no match
+	// -- results wrong)
 	const uint32_t dg = a.diag;
 #else
 	constexpr uint32_t dg = 0;
@@ -78,6 +91,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const uint32_t qbits = rfl(a.qt_bits), qseed = rfl(a.qt_seed);
 	const uint32_t rsh = 32 - qbits, rmask = (1u << rsh) - 1;
 	const bool dlive = a.qt_live == M_DST;   // the one live key: dst (else src)
+#if XFG_QT_BKPOL != 0
+	// (A/B: the bucket loads as buffer loads with cache policy XFG_QT_BKAUX)
+	const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+		(void *)a.qt, 0, (int)((32ull << qbits) < 0x7fffffffull ? (32ull << qbits) : 0x7fffffffull), 0x00020000);
+#endif
 	const bool klive = a.t4.count != 0;
 	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
 	cn.init(a, tid, NT);
@@ -159,7 +177,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
 				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
 							 : reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
+#if XFG_QT_WIN_NT
 				pre[it] = __builtin_nontemporal_load(src);
+#else
+				pre[it] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>((uintptr_t)src);
+#endif
 			}
 			plen = *reinterpret_cast<const __attribute__((address_space(1))) len_t *>(
 				lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
@@ -201,7 +223,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// ---- R: tile k-1's bucket -> CHECK_MAP (xdpfilt_prog.h:56-64)
 		const uint32_t r_act = pk_act(r_pk), r_ps = pk_ps(r_pk), w_len = pk_len(r_pk);
 		uint32_t w_act = A_NONE, w_tag = CT_NONE, w_ps = r_ps;
-		if (vR) {
+		if (vR && !(dg & 8192)) {
 			// 16 entries, filled in order; keys are unique, so at most one
 			// matches.  A miss in a bucket marked overflowed may be a key
 			// that did not fit: the canonical table decides it (deferred).
@@ -240,8 +262,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			if (w_act <= A_PASS && !(dg & 8))
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
 			count((dg & 1) ? CT_NONE : w_tag, (dg & 1) ? XFG_PORT_TAB : w_ps);
-			stat(w_act, w_len);
-			const unsigned long long dm = __ballot(w_act == A_DEFER);
+			if (!(dg & 128))
+				stat(w_act, w_len);
+			const unsigned long long dm = (dg & 128) ? 0ull : __ballot(w_act == A_DEFER);
 			if (dm) {
 				const uint32_t pos = ndef + lanes_below(dm);
 				if (w_act == A_DEFER)
@@ -259,15 +282,21 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		if (vP) {
 			const uint32_t rem = n - tP * 64 >= 64 ? 64u : n - tP * 64;
 			__builtin_amdgcn_wave_barrier();
+			if (!(dg & 32)) {
 #pragma unroll
-			for (int it = 0; it < CPP; it++) {
-				const int c = it * 64 + lane;
-				const int pk = c / CPP, sub = c % CPP;
-				uint32_t *dst = &rows[pk * ROWDW + sub * 4];
-				dst[0] = cur[it].x;
-				dst[1] = cur[it].y;
-				dst[2] = cur[it].z;
-				dst[3] = cur[it].w;
+				for (int it = 0; it < CPP; it++) {
+					const int c = it * 64 + lane;
+					const int pk = c / CPP, sub = c % CPP;
+					uint32_t *dst = &rows[pk * ROWDW + sub * 4];
+					dst[0] = cur[it].x;
+					dst[1] = cur[it].y;
+					dst[2] = cur[it].z;
+					dst[3] = cur[it].w;
+				}
+			} else {   // (diagnostics: the data kept live, not staged)
+#pragma unroll
+				for (int it = 0; it < CPP; it++)
+					asm volatile("" ::"v"(cur[it]));
 			}
 			len = (uint32_t)lane < rem ? min((uint32_t)curlen, a.stride) : 0u;
 			__builtin_amdgcn_wave_barrier();
@@ -292,15 +321,28 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 		if (!(dg & 2)) {
 			const auto ab = __builtin_amdgcn_permlane32_swap(lbk, lbk, false, false);
+#if XFG_QT_BKPOL == 0
 			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
 			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
 			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
+#else
+			const uint32_t ho = (uint32_t)(lane >> 5) * 16;
+			bk0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ho + (ab[0] << 5), 0, XFG_QT_BKAUX);
+			bk1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ho + (ab[1] << 5), 0, XFG_QT_BKAUX);
+#endif
 		}
 		__builtin_amdgcn_sched_barrier(0);
 #endif
 		PMARK("P");
 		// ---- P: parse tile k, hash its key, plan its fallback
-		if (vP) {
+		if (vP && (dg & 64)) {   // (diagnostics: no parse)
+			const uint32_t gi = tP * 64 + lane;
+			r_b = pick(gi < n, hk >> rsh, 0u);
+			r_key = XFG_QT_USED | (hk & rmask);
+			r_sel = gi < n;
+			r_pk = pk3(pick(gi < n, MISS, A_NONE), XFG_PORT_TAB, len);
+			r_tag = CT_NONE;
+		} else if (vP) {
 			const uint32_t gi = tP * 64 + lane;
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
