@@ -12,7 +12,8 @@ rule sets with keys whose flags lack the live mask, the zero key, both
 window sizes and a non-dense stride, ports beside the index, buckets that
 overflow (their misses and their spilled keys decided by the canonical
 table), rebuilds after inserts / deletes / flag changes between batches,
-and rule sets where the index must NOT apply (both directions live).
+both IPv4 directions live (one image for src|dst rule sets, two
+otherwise), and single edits patched into the index between batches.
 """
 import numpy as np
 import pytest
@@ -185,11 +186,63 @@ def test_qt_rebuilt_after_rule_changes(G):
     f.close()
 
 
-def test_qt_not_taken_with_both_directions_live(G):
-    rules, v4, ports = one_direction_rules(51, 5000, 2)
-    rules.v4_vals[:10] = 1                          # a src rule: both directions live
-    data, lens = X.gen_workload(52, 3, 1 << 15, 64, v4=v4, ports=ports)
-    run_both(G, "xdpfilt_dny_all", rules, data, lens, 64, path=2)
+def both_direction_traffic(seed, n, v4, ports, stride=64):
+    """C3-shaped traffic with ruled destinations, a ruled source in a
+    quarter of the IPv4 frames (some with a ruled destination too: the dst
+    lookup decides those), and the structured fuzz corpus."""
+    d1, l1 = X.gen_workload(seed, 3, n, stride, v4=v4, ports=ports)
+    d = d1.reshape(-1, stride)
+    ip4 = np.nonzero((d[:, 12] == 8) & (d[:, 13] == 0))[0][::4]
+    d[ip4, 26:30] = v4[(np.arange(len(ip4)) * 7919) % len(v4)]
+    return d1, l1
+
+
+@pytest.mark.parametrize("variant", ["xdpfilt_dny_all", "xdpfilt_alw_ip"])
+@pytest.mark.parametrize("shape", ["sym", "asym"])
+@pytest.mark.parametrize("stride", [64, 128])
+def test_qt_both_directions(G, variant, shape, stride):
+    """Both IPv4 lookups through the index (lookup_verdict_ipv4,
+    xdpfilt_prog.h:121-134: dst first, then src; only the first hit
+    counts).  sym: every ruled key carries src|dst (`xdp-filter ip -m
+    src,dst`), one image serves both lookups; asym: keys with dst only, src
+    only, both, and proto bits only -- two images."""
+    rules, v4, ports = one_direction_rules(51, 20000, 3)
+    if shape == "asym":
+        rng = np.random.default_rng(52)
+        f = rules.v4_vals & ~np.uint64(3)
+        pick = rng.integers(0, 4, len(v4)).astype(np.uint64)   # 0: proto only
+        rules.v4_vals = f | pick
+    d1, l1 = both_direction_traffic(53, 1 << 16, v4, ports, stride)
+    d2, l2 = fuzz_at(54, 1 << 15, stride, rules, ports)
+    data, lens = np.concatenate([d1, d2]), np.concatenate([l1, l2])
+    run_both(G, variant, rules, data, lens, stride)
+
+
+def test_qt_both_directions_single_edits(G):
+    """Single edits on a both-direction index: patched in place within one
+    shape, rebuilt when a key with one direction first appears in a
+    one-image index."""
+    variant = "xdpfilt_dny_all"
+    feat = X.VARIANT_FEATURES[variant]
+    rules, v4, ports = one_direction_rules(61, 20000, 3)
+    f = make_filter(G, variant, qt_min_keys=1, ipv4_capacity=1 << 16)
+    f.load_rules(rules)
+    cur = rules.prepared().copy()
+    rng = np.random.default_rng(62)
+    for step, newflag in enumerate([3, 0, 2, 1, 3]):
+        d, l = both_direction_traffic(63 + step, 1 << 15, cur.v4_keys, ports)
+        v = f.run(d, l, stride=64)
+        assert f.last_path() == 5
+        ov, cur, ost = X.run_oracle(feat, d, l, cur, stride=64)
+        got = gpu_values(f, G, cur)
+        assert_same(v, got, f.stats(), ov, cur, ost)
+        f.stats_reset()
+        idx = rng.choice(len(cur.v4_keys), 30, replace=False)
+        for i in idx:   # 30 single edits: flags to newflag (counts kept)
+            val = (int(cur.v4_vals[i]) & ~3) | newflag
+            f.update(G.MAP_IPV4, bytes(cur.v4_keys[i]), val)
+            cur.v4_vals[i] = val
+    f.close()
 
 
 def test_qt_counts_folded_across_batches_and_writes(G):

@@ -81,7 +81,7 @@ struct xfg_dev {
 	 * under d->lock */
 	uint32_t *qt_img, *qt_trans;
 	uint64_t qt_img_bytes, qt_trans_bytes;
-	uint32_t qt_gen, qt_bits, qt_seed, qt_live, qt_n;
+	uint32_t qt_gen, qt_bits, qt_seed, qt_live, qt_n, qt_nimg;
 	/* the count kernel's QT-order hit counts (xfg_kargs.qt_hits) and
 	 * whether a launch may have added to them since the last fold */
 	unsigned long long *qt_hits;
@@ -693,8 +693,21 @@ static int qt_edit(xfg_ctx *ctx, uint64_t slot, const void *key, uint8_t old, ui
 	struct xfg_qt *q = &ctx->qt;
 	if (ctx->qt_dirty || !ctx->qt_gen || !q->img)
 		return 0;   /* (rebuilt before its next use anyway) */
-	const int was = (old & q->live) == q->live, is = (nw & q->live) == q->live;
-	if (was == is)
+	/* per image: does the key enter or leave it */
+	int chg[2] = { 0, 0 }, any = 0;
+	for (uint32_t im = 0; im < q->nimg; im++) {
+		const uint32_t mk = xfg_qt_img_mask(q->live, q->nimg, im);
+		const int was = (old & mk) == mk, is = (nw & mk) == mk;
+		chg[im] = was == is ? 0 : (is ? 1 : -1);
+		any |= chg[im];
+	}
+	/* one image for both directions holds only keys with both or neither:
+	 * a key with exactly one direction needs the second image (rebuild) */
+	if (q->live == 3 && q->nimg == 1 && ((nw & 3) == 1 || (nw & 3) == 2)) {
+		ctx->qt_dirty = 1;
+		return 0;
+	}
+	if (!any)
 		return 0;
 	if (xfg_qt_bits_for(ctx->t[0].count) != q->bits) {
 		ctx->qt_dirty = 1;
@@ -707,7 +720,10 @@ static int qt_edit(xfg_ctx *ctx, uint64_t slot, const void *key, uint8_t old, ui
 		ctx->qt_dirty = 1;
 		return 0;
 	}
-	const uint32_t b = xfg_qt_patch(q, k, (uint32_t)slot, is);
+	uint32_t bk[2] = { 0, 0 };
+	for (uint32_t im = 0; im < q->nimg; im++)
+		if (chg[im])
+			bk[im] = xfg_qt_patch(q, im, k, (uint32_t)slot, chg[im] > 0);
 	uint32_t gen = ctx->qt_gen + 1;
 	if (!gen)
 		gen = 1;
@@ -716,11 +732,15 @@ static int qt_edit(xfg_ctx *ctx, uint64_t slot, const void *key, uint8_t old, ui
 		struct xfg_dev *d = &ctx->dev[i];
 		pthread_mutex_lock(&d->lock);
 		if (d->qt_gen == ctx->qt_gen) {
-			int e = dev_write(d, (uint8_t *)d->qt_img + (uint64_t)b * XFG_QT_BUCKET,
-					  q->img + (uint64_t)b * XFG_QT_SLOTS, XFG_QT_BUCKET);
-			if (!e)
-				e = dev_write(d, d->qt_trans + (uint64_t)b * XFG_QT_SLOTS,
-					      q->trans + (uint64_t)b * XFG_QT_SLOTS, XFG_QT_SLOTS * 4);
+			int e = 0;
+			for (uint32_t im = 0; im < q->nimg && !e; im++) {
+				if (!chg[im])
+					continue;
+				const uint64_t o = (uint64_t)im * q->nslots + (uint64_t)bk[im] * XFG_QT_SLOTS;
+				e = dev_write(d, (uint8_t *)d->qt_img + o * 2, q->img + o, XFG_QT_BUCKET);
+				if (!e)
+					e = dev_write(d, d->qt_trans + o, q->trans + o, XFG_QT_SLOTS * 4);
+			}
 			if (!e)
 				d->qt_gen = gen;
 			else if (!err)
@@ -1273,7 +1293,8 @@ static int qt_refresh(xfg_ctx *ctx, struct xfg_dev *d, uint32_t live)
 	}
 	if (d->qt_gen == ctx->qt_gen)
 		return 0;
-	const uint64_t ib = (1ull << ctx->qt.bits) * XFG_QT_BUCKET, tb = (uint64_t)ctx->qt.nslots * 4;
+	const uint64_t ib = (uint64_t)ctx->qt.nimg * (1ull << ctx->qt.bits) * XFG_QT_BUCKET;
+	const uint64_t tb = (uint64_t)ctx->qt.nimg * ctx->qt.nslots * 4;
 	pthread_mutex_lock(&d->lock);
 	if (!(err = qt_fold_locked(d)) &&   /* (through the index being replaced) */
 	    !(err = scratch(d, (void **)&d->qt_img, &d->qt_img_bytes, ib)) &&
@@ -1284,7 +1305,8 @@ static int qt_refresh(xfg_ctx *ctx, struct xfg_dev *d, uint32_t live)
 		d->qt_bits = ctx->qt.bits;
 		d->qt_seed = ctx->qt.seed;
 		d->qt_live = ctx->qt.live;
-		d->qt_n = ctx->qt.nslots;
+		d->qt_nimg = ctx->qt.nimg;
+		d->qt_n = ctx->qt.nimg * ctx->qt.nslots;
 	}
 	pthread_mutex_unlock(&d->lock);
 	return err;
@@ -1369,9 +1391,10 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	 * map large enough that the prefilter + bucket-line chain leaves L2;
 	 * its hit log must fit the count kernel's histogram */
 	if (a->pipe && a->km && !a->split) {
+		/* (both directions live: up to two images, twice the QT slots) */
 		const int dl = a->t4.count && (a->t4.fmask & 2), sl = a->t4.count && (a->t4.fmask & 1);
-		const int ok = (dl ^ sl) && !ctx->flag_cnt[0][7] &&
-			       qt_hist_fits(xfg_qt_bits_for(a->t4.count));
+		const int ok = (dl | sl) && !ctx->flag_cnt[0][7] &&
+			       qt_hist_fits(xfg_qt_bits_for(a->t4.count) + (dl & sl));
 		int use = ok && a->t4.count >= ctx->qt_min_keys;
 #ifdef XFG_DIAG
 		const char *qo = getenv("XFG_QT");   /* "off" / "on" (any size) */
@@ -1381,7 +1404,7 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 			use = ok;
 #endif
 		if (use) {
-			int err2 = qt_refresh(ctx, d, dl ? 2u : 1u);
+			int err2 = qt_refresh(ctx, d, (dl ? 2u : 0u) | (sl ? 1u : 0u));
 			if (err2)
 				return err2;
 			a->qt = d->qt_img;   /* (parameters: launch_batch, under d->lock) */
@@ -1466,6 +1489,10 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.qt_seed = d->qt_seed;
 		a.qt_live = d->qt_live;
 		a.qt_n = d->qt_n;
+		/* the second (src) lookup's image and its slots' offset: the same
+		 * image at offset 0 when one serves both directions */
+		a.qt_base = d->qt_nimg == 2 ? d->qt_n / 2 : 0;
+		a.qt2 = d->qt_img + (uint64_t)a.qt_base * 2 / 4;
 		/* its QT-order counts (zeroed when (re)allocated; a resize only
 		 * follows a fold: qt_refresh) */
 		const uint64_t qb = (uint64_t)d->qt_n * 8, had = d->qt_hits_bytes;

@@ -1343,17 +1343,27 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	}
 }
 
+template <uint32_t FEAT, bool L16, bool BOTH>
+void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
+{
+	if (a.window <= 64 && a.dense)
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+	else if (a.window <= 64)
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+	else if (a.dense)
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+	else
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+}
+
+// (qt_live 3: both IPv4 lookups through the index)
 template <uint32_t FEAT, bool L16>
 void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
-	if (a.window <= 64 && a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
-	else if (a.window <= 64)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
-	else if (a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+	if (a.qt_live == 3)
+		launch_pipeq2<FEAT, L16, true>(a, grid, dl, s);
 	else
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+		launch_pipeq2<FEAT, L16, false>(a, grid, dl, s);
 }
 
 template <uint32_t FEAT>
@@ -1490,8 +1500,8 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 		} else if (kind == 5) {
 			done = true;
 			e = window <= 64
-				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true>, QT_THREADS(64), dyn)
-				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true>, QT_THREADS(128), dyn);
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true, false>, QT_THREADS(64), dyn)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true, false>, QT_THREADS(128), dyn);
 		}
 	}
 	if (done)

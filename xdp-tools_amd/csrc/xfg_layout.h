@@ -189,10 +189,15 @@ struct xfg_kargs {
 	uint32_t grid_parse;
 	uint32_t bloom_off;
 	uint32_t *rec_ka, *rec_kb, *rec_port;
-	/* Quotient index of the IPv4 map (NULL = none): 1 << qt_bits buckets;
-	 * its slots are counter identities qt_base + slot (after the ports),
-	 * mapped to canonical ones by qt_trans; qt_live = the one live mask */
+	/* Quotient index of the IPv4 map (NULL = none): 1 << qt_bits buckets
+	 * per image; QT slot bucket * 16 + entry of image 0 (at qt), and
+	 * qt_base + bucket * 16 + entry of the second lookup's image (at qt2),
+	 * mapped to canonical slots by qt_trans.  qt_live: the live mask, 2
+	 * (dst) or 1 (src) for one lookup, 3 for both (dst in image 0, src in
+	 * qt2: image 1, or image 0 itself with qt_base 0 when every ruled key
+	 * carries both directions) */
 	const uint32_t *qt;
+	const uint32_t *qt2;
 	const uint32_t *qt_trans;
 	/* hit counts of the QT slots (qt_n, QT-slot order): the count kernel
 	 * adds there, the host folds them into the canonical counters through

@@ -51,12 +51,27 @@
 #ifndef XFG_QT_WIN_NT
 #define XFG_QT_WIN_NT 1
 #endif
+// (A/B: verdict bytes packed four to a dword store (1) or a byte per lane (0);
+// non-temporal (1) or plain (0))
+#ifndef XFG_QT_VPACK
+#define XFG_QT_VPACK 0
+#endif
+// (A/B: tile k-1's verdict and hit-log stores issued last in the iteration,
+// after tile k+2's loads, as a fixed two instructions -- so that the next
+// iteration's one wait does not wait for their write acknowledgements)
+#ifndef XFG_QT_LATE
+#define XFG_QT_LATE 0
+#endif
+#ifndef XFG_QT_VNT
+#define XFG_QT_VNT 1
+#endif
 
 namespace {
 
-template <uint32_t FEAT, int W, bool DENSE, bool L16>
+template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH>
 __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
+	static_assert(!BOTH || XFG_QT_EARLY_L, "both directions: the keys are hashed before the parse");
 	static_assert((FEAT & F_IPV4) != 0, "IPv4-key mode needs the IPv4 feature");
 	constexpr int NW = QT_WAVES(W);
 	constexpr int NT = 64 * NW;
@@ -78,8 +93,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// (diagnostics: 1 no counting, 2 no bucket loads, 8 no verdict stores,
 	// 16 no workgroup-end partition, 32 no LDS row staging, 64 no parse, 128
 	// no stats or deferral lists, 2048 no deferred packets, 4096 hits as
-	// memory-side atomics into scratch instead of the hit log, 8192 no match
-	// -- results wrong)
+	// memory-side atomics into scratch instead of the hit log, 8192 no match,
+	// 16384 no hit-log store -- results wrong)
 	const uint32_t dg = a.diag;
 #else
 	constexpr uint32_t dg = 0;
@@ -90,11 +105,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const uint64_t qb = rfl64((uint64_t)(uintptr_t)a.qt);
 	const uint32_t qbits = rfl(a.qt_bits), qseed = rfl(a.qt_seed);
 	const uint32_t rsh = 32 - qbits, rmask = (1u << rsh) - 1;
-	const bool dlive = a.qt_live == M_DST;   // the one live key: dst (else src)
+	const bool dlive = BOTH || a.qt_live == M_DST;   // the one live key: dst (else src)
+	// (both directions: the src lookup's image and its QT slots' offset)
+	const uint64_t qb2 = BOTH ? rfl64((uint64_t)(uintptr_t)a.qt2) : 0;
+	const uint32_t qbase2 = BOTH ? rfl(a.qt_base) : 0u;
 #if XFG_QT_BKPOL != 0
 	// (A/B: the bucket loads as buffer loads with cache policy XFG_QT_BKAUX)
 	const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
-		(void *)a.qt, 0, (int)((32ull << qbits) < 0x7fffffffull ? (32ull << qbits) : 0x7fffffffull), 0x00020000);
+		(void *)a.qt, 0, (int)((64ull << qbits) < 0x7fffffffull ? (64ull << qbits) : 0x7fffffffull), 0x00020000);
 #endif
 	const bool klive = a.t4.count != 0;
 	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
@@ -130,7 +148,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			if (q)
 				atomicAdd(reinterpret_cast<uint32_t *>(a.pbuf) + qs, 1u);
 		} else {
-			log_append(tregion, tn, pick(q, qs, CT_NONE), lane);
+			if (!(dg & 16384))   // (diagnostics: no hit-log store)
+				log_append(tregion, tn, pick(q, qs, CT_NONE), lane);
 			if (q)
 				atomicAdd(&s_lh[log_part(qs)], 1u);
 		}
@@ -155,6 +174,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		st_b2 += pick(act == A_PASS, len, 0u);
 	};
 	uint32_t ndef = 0;
+#if XFG_QT_VPACK
+	const bool vpk = ((uintptr_t)a.verdicts & 3) == 0;
+#endif
 
 	// windows + lengths of tile t (clamped to the last tile): CPP + 1 loads,
 	// always issued
@@ -208,12 +230,48 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	uint32_t r_key = 0, r_b = 0, r_pk = pk3(A_NONE, XFG_PORT_TAB, 0), r_tag = CT_NONE;
 	bool r_sel = false;
 	u32x4 bk0 = { 0, 0, 0, 0 }, bk1 = { 0, 0, 0, 0 };
-
+	// (both directions: the src key's entry, bucket and bucket halves)
+	uint32_t r_key2 = 0, r_b2 = 0;
+	u32x4 bs0 = { 0, 0, 0, 0 }, bs1 = { 0, 0, 0, 0 };
+	// one bucket's 16 entries (halves in lanes i and i + 32 of h0 / h1, see
+	// L) searched for entry q: found, its index, the overflow marker
+	auto match = [](const u32x4 &h0, const u32x4 &h1, uint32_t q, bool &found, uint32_t &ix) {
+		uint32_t w[8];
+#pragma unroll
+		for (int c = 0; c < 4; c++) {
+			const auto sw = __builtin_amdgcn_permlane32_swap(h0[c], h1[c], false, false);
+			w[c] = sw[0];
+			w[4 + c] = sw[1];
+		}
+		found = false;
+		ix = 0;
+#pragma unroll
+		for (int i = 0; i < 8; i++) {
+			const bool lo = (w[i] & 0xffffu) == q, hi = (w[i] >> 16) == q;
+			found |= lo | hi;
+			ix = pick(lo, 2u * i, ix);
+			ix = pick(hi, 2u * i + 1, ix);
+		}
+		return (w[7] >> 16) == XFG_QT_OVF_MARK;
+	};
+#if XFG_QT_LATE
+	// the late stores' lanes: verdict address / byte, log position / entry
+	uint32_t ls_gi = 0, ls_act = 0, ls_pos = 0, ls_val = 0;
+	// (iteration 0 -- the only one without a tile to resolve -- is peeled:
+	// every later one resolves a tile and ends with exactly two stores, so
+	// the wait that ends an iteration has a fixed count)
+	auto iteration = [&](auto peel_c, uint32_t k, u32x4 (&cur)[CPP], len_t &curlen) {
+		constexpr bool PEEL = decltype(peel_c)::value;
+		const uint32_t tP = first + k * step;
+		const bool vP = tP < nt;
+		constexpr bool vR = !PEEL;   // (k >= 1: tile first + (k-1) step < nt)
+#else
 	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen) {
 		const uint32_t tP = first + k * step;
 		const bool vP = tP < nt;
 		const bool vR = k >= 1 && tP - step < nt;
 		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
+#endif
 		// (the length is used from here on: without this the compiler
 		// rotates its zero-extension to the previous iteration's end, where
 		// it waits for the load -- and every older one -- early)
@@ -227,29 +285,28 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			// 16 entries, filled in order; keys are unique, so at most one
 			// matches.  A miss in a bucket marked overflowed may be a key
 			// that did not fit: the canonical table decides it (deferred).
-			const uint32_t q = r_key;
 			// the halves to their packet's lane (see L): lane i < 32 holds
 			// half 0 of packet i in bk0 and half 1 of packet i in lane
 			// i + 32 of bk0; lanes i + 32 likewise in bk1 for packet 32 + i
-			uint32_t w[8];
-#pragma unroll
-			for (int c = 0; c < 4; c++) {
-				const auto sw = __builtin_amdgcn_permlane32_swap(bk0[c], bk1[c], false, false);
-				w[c] = sw[0];
-				w[4 + c] = sw[1];
-			}
-			bool found = false;
-			uint32_t ix = 0;
-#pragma unroll
-			for (int i = 0; i < 8; i++) {
-				const bool lo = (w[i] & 0xffffu) == q, hi = (w[i] >> 16) == q;
-				found |= lo | hi;
-				ix = pick(lo, 2u * i, ix);
-				ix = pick(hi, 2u * i + 1, ix);
-			}
+			bool found;
+			uint32_t ix;
+			const bool ovf = match(bk0, bk1, r_key, found, ix);
 			found &= r_sel;
-			const bool defer = r_sel & !found & ((w[7] >> 16) == XFG_QT_OVF_MARK);
-			const uint32_t slot = r_b * XFG_QT_SLOTS + ix;
+			bool defer = r_sel & !found & ovf;
+			uint32_t slot = r_b * XFG_QT_SLOTS + ix;
+			if constexpr (BOTH) {
+				// lookup_verdict_ipv4 (xdpfilt_prog.h:121-134): the src
+				// key only when the dst key decided nothing -- the first
+				// matching lookup's counter alone is bumped
+				bool f2;
+				uint32_t ix2;
+				const bool ovf2 = match(bs0, bs1, r_key2, f2, ix2);
+				const bool open = r_sel & !found & !defer;
+				f2 &= open;
+				defer |= open & !f2 & ovf2;
+				slot = pick(f2, qbase2 + r_b2 * XFG_QT_SLOTS + ix2, slot);
+				found |= f2;
+			}
 			w_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
 			w_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, r_tag));
 			w_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
@@ -257,10 +314,80 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 
 		PMARK("W");
 		// ---- W: verdicts, counters, stats, deferrals of tile k-1
+#if XFG_QT_LATE
+		if (vR) {
+			const uint32_t tb = (tP - step) * 64, gi = tb + lane;
+			// verdict: every lane stores (a fixed instruction): a deferred
+			// lane a placeholder the deferred pass overwrites, a lane past
+			// the batch's end lane 0's byte at lane 0's address
+			const uint32_t a0 = __builtin_amdgcn_readfirstlane(w_act);
+			ls_gi = pick(gi < n, gi, tb);
+			ls_act = pick(gi < n, w_act, a0);
+			// hit log: a block of 64 entries at tn, the hits first, then
+			// CT_NONE padding the next block overwrites (the count advances
+			// by the hits only; a wave's region has room: tn + 64 <= its
+			// packets so far + 64 <= defer_cap)
+			const bool q = (w_tag != CT_NONE) & ((w_tag & QTAG) != 0) & !(dg & 1);
+			const unsigned long long m = __ballot(q);
+			ls_pos = tn + pick(q, lanes_below(m), (uint32_t)__popcll(m) + lanes_below(~m));
+			ls_val = pick(q, w_tag & ~QTAG, CT_NONE);
+			tn += (uint32_t)__popcll(m);
+			if (q)
+				atomicAdd(&s_lh[log_part(w_tag & ~QTAG)], 1u);
+			const uint32_t ctag = (dg & 1) ? CT_NONE : pick(q, CT_NONE, w_tag);
+			const uint32_t cps = (dg & 1) ? XFG_PORT_TAB : w_ps;
+			if constexpr (PORTS)
+				if (cps < XFG_PORT_TAB)
+					atomicAdd(&s_pcnt[cps], 1u);
+			const bool dc = (ctag != CT_NONE) & (ctag < a.dcnt) & !(cps < XFG_PORT_TAB);
+			if (dc)
+				atomicAdd(&cn.dcnt[ctag], 1u);
+			cn.bump(a, pick(dc | (cps < XFG_PORT_TAB), CT_NONE, ctag), lane);
+			if (!(dg & 128))
+				stat(w_act, w_len);
+			const unsigned long long dm = (dg & 128) ? 0ull : __ballot(w_act == A_DEFER);
+			if (dm) {
+				const uint32_t pos = ndef + lanes_below(dm);
+				if (w_act == A_DEFER)
+					gst32(dlist + pos, gi);
+				ndef += (uint32_t)__popcll(dm);
+			}
+		}
+#else
 		if (vR) {
 			const uint32_t gi = (tP - step) * 64 + lane;
-			if (w_act <= A_PASS && !(dg & 8))
+#if XFG_QT_VPACK
+			// a whole tile's 64 verdict bytes as 16 dwords (lanes 4j, the
+			// bytes of lanes 4j..4j+3 gathered by DPP): a deferred lane's
+			// byte is a placeholder the deferred pass overwrites
+			if (!(dg & 8)) {
+				const uint32_t tb = (tP - step) * 64;
+				if (vpk & (n - tb >= 64)) {
+					const uint32_t b = w_act & 0xffu;
+					const uint32_t x = b | ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 249, 0xf, 0xf, false) << 8) |
+							   ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 254, 0xf, 0xf, false) << 16) |
+							   ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 255, 0xf, 0xf, false) << 24);
+					if ((lane & 3) == 0) {
+						auto *vp = reinterpret_cast<__attribute__((address_space(1))) uint32_t *>(
+							(uintptr_t)(a.verdicts + gi));
+#if XFG_QT_VNT
+						__builtin_nontemporal_store(x, vp);
+#else
+						*vp = x;
+#endif
+					}
+				} else if (w_act <= A_PASS)
+					__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
+			}
+#else
+			if (w_act <= A_PASS && !(dg & 8)) {
+#if XFG_QT_VNT
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
+#else
+				*reinterpret_cast<__attribute__((address_space(1))) uint8_t *>((uintptr_t)(a.verdicts + gi)) = (uint8_t)w_act;
+#endif
+			}
+#endif
 			count((dg & 1) ? CT_NONE : w_tag, (dg & 1) ? XFG_PORT_TAB : w_ps);
 			if (!(dg & 128))
 				stat(w_act, w_len);
@@ -272,6 +399,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
+#endif
 
 		PMARK("S");
 		// ---- S: tile k's windows into the rows, lengths clamped to the
@@ -312,12 +440,16 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// looked up once); R moves them to the packet's lane.  Every lane
 		// loads (a fixed count); one whose frame is not IPv4 loads bucket 0
 		// (a shared line).
-		uint32_t hk = 0, lbk = 0;
+		uint32_t hk = 0, lbk = 0, hk2 = 0, lbk2 = 0;
 		if (vP) {
 			const uint32_t e3 = myrow[3], e6 = myrow[6], e7 = myrow[7], e8 = myrow[8];
 			const uint32_t key = dlive ? __builtin_amdgcn_alignbyte(e8, e7, 2) : __builtin_amdgcn_alignbyte(e7, e6, 2);
 			hk = xfg_qt_hash(key, qseed);
 			lbk = pick((e3 & 0xffffu) == 0x0008u, hk >> rsh, 0u);
+			if constexpr (BOTH) {   // the src key (saddr, bytes 26..29)
+				hk2 = xfg_qt_hash(__builtin_amdgcn_alignbyte(e7, e6, 2), qseed);
+				lbk2 = pick((e3 & 0xffffu) == 0x0008u, hk2 >> rsh, 0u);
+			}
 		}
 		if (!(dg & 2)) {
 			const auto ab = __builtin_amdgcn_permlane32_swap(lbk, lbk, false, false);
@@ -325,10 +457,22 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
 			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
 			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
+			if constexpr (BOTH) {
+				const auto ab2 = __builtin_amdgcn_permlane32_swap(lbk2, lbk2, false, false);
+				const uint64_t hb2 = qb2 + (uint64_t)(lane >> 5) * 16;
+				bs0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[0] << 5));
+				bs1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[1] << 5));
+			}
 #else
 			const uint32_t ho = (uint32_t)(lane >> 5) * 16;
 			bk0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ho + (ab[0] << 5), 0, XFG_QT_BKAUX);
 			bk1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ho + (ab[1] << 5), 0, XFG_QT_BKAUX);
+			if constexpr (BOTH) {
+				const auto ab2 = __builtin_amdgcn_permlane32_swap(lbk2, lbk2, false, false);
+				const uint32_t ob = qbase2 * 2;   // (image 1's byte offset: 0 with one image)
+				bs0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ob + ho + (ab2[0] << 5), 0, XFG_QT_BKAUX);
+				bs1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ob + ho + (ab2[1] << 5), 0, XFG_QT_BKAUX);
+			}
 #endif
 		}
 		__builtin_amdgcn_sched_barrier(0);
@@ -356,6 +500,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			r_b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
 			r_key = XFG_QT_USED | (h & rmask);
 			r_sel = kok;
+			if constexpr (BOTH) {
+				r_b2 = pick(kok, hk2 >> rsh, 0u);
+				r_key2 = XFG_QT_USED | (hk2 & rmask);
+			}
 			uint32_t fa = pick(r.abort_at != NST, A_ABORTED, MISS), ft = CT_NONE, fs = XFG_PORT_TAB;
 			if constexpr (PORTS) {
 				if (a.port_count) {
@@ -413,6 +561,19 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		__builtin_amdgcn_sched_barrier(0);
 		issue(tP + 2 * step, cur, curlen);
 		__builtin_amdgcn_sched_barrier(0);
+#if XFG_QT_LATE
+		if constexpr (!PEEL) {
+			__builtin_nontemporal_store((uint8_t)ls_act,
+				reinterpret_cast<__attribute__((address_space(1))) uint8_t *>((uintptr_t)(a.verdicts + ls_gi)));
+			gst32(tregion + ls_pos, ls_val);
+			__builtin_amdgcn_sched_barrier(0);
+			// the next iteration's data: everything but tile k+2's loads
+			// and these two stores
+			__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 3) & 15) | (((CPP + 3) >> 4) << 14));
+		} else {
+			__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
+		}
+#endif
 	};
 
 	u32x4 preA[CPP], preB[CPP];
@@ -424,6 +585,19 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		__builtin_amdgcn_sched_barrier(0);
 	}
 	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 2 : 0u;
+#if XFG_QT_LATE
+	if (iters) {   // (iters >= 2 whenever the wave has a tile)
+		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
+		iteration(std::true_type{}, 0, preA, lenA);
+		uint32_t k = 1;
+		for (; k + 1 < iters; k += 2) {
+			iteration(std::false_type{}, k, preB, lenB);
+			iteration(std::false_type{}, k + 1, preA, lenA);
+		}
+		if (k < iters)
+			iteration(std::false_type{}, k, preB, lenB);
+	}
+#else
 	uint32_t k = 0;
 	for (; k + 1 < iters; k += 2) {
 		iteration(k, preA, lenA);
@@ -431,9 +605,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	}
 	if (k < iters)
 		iteration(k, preA, lenA);
+#endif
 
 	if (dg & 2048)
 		ndef = 0;
+#if XFG_QT_VPACK || XFG_QT_LATE
+	if (ndef)   // (the placeholder bytes of the packed / late stores land first)
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 	// the deferred packets: the whole reference walk over the canonical
 	// table (classify_staged), 64 at a time
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {

@@ -258,51 +258,35 @@ void xfg_qt_free(struct xfg_qt *q)
 	q->trans = NULL;
 }
 
-int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *flags,
-		 uint32_t live, uint32_t seed)
+/* Image @im of @q (mask @mask): keys homed per bucket first -- a bucket
+ * that more than XFG_QT_SLOTS keys home in holds XFG_QT_SLOTS - 1 of them
+ * and the overflow marker. */
+static int qt_build_img(struct xfg_qt *q, uint32_t im, const struct xfg_table *t,
+			const uint8_t *flags, uint32_t mask)
 {
-	if (t->keylen != 4)
-		return -EINVAL;
-	const uint32_t bits = xfg_qt_bits_for(t->count);
-	const uint64_t nb = 1ull << bits, ns = nb * XFG_QT_SLOTS;
-	if (q->bits != bits || !q->img) {
-		xfg_qt_free(q);
-		q->img = malloc(nb * XFG_QT_BUCKET);
-		q->trans = malloc(ns * 4);
-		if (!q->img || !q->trans) {
-			xfg_qt_free(q);
-			return -ENOMEM;
-		}
-	}
-	memset(q->img, 0, nb * XFG_QT_BUCKET);
-	memset(q->trans, 0xff, ns * 4);
-	q->bits = bits;
-	q->seed = seed;
-	q->live = live;
-	q->nslots = (uint32_t)ns;
-	q->placed = q->spilled = 0;
-	const uint32_t rbits = 32 - bits, rmask = (1u << rbits) - 1;
-	/* keys homed per bucket first: a bucket that more than XFG_QT_SLOTS
-	 * keys home in holds XFG_QT_SLOTS - 1 of them and the overflow marker */
+	const uint64_t nb = 1ull << q->bits;
+	uint16_t *img = q->img + (uint64_t)im * q->nslots;
+	uint32_t *trans = q->trans + (uint64_t)im * q->nslots;
+	const uint32_t rbits = 32 - q->bits, rmask = (1u << rbits) - 1;
 	uint8_t *homed = calloc(nb, 1);
 	if (!homed)
 		return -ENOMEM;
 	for (int64_t s = xfg_table_next_slot(t, -1); s >= 0; s = xfg_table_next_slot(t, s)) {
-		if ((flags[s] & live) != live)
+		if ((flags[s] & mask) != mask)
 			continue;
 		uint32_t k;
 		xfg_table_slot_key(t, (uint64_t)s, &k);
-		const uint32_t b = xfg_qt_hash(k, seed) >> rbits;
+		const uint32_t b = xfg_qt_hash(k, q->seed) >> rbits;
 		if (homed[b] < 255)
 			homed[b]++;
 	}
 	for (int64_t s = xfg_table_next_slot(t, -1); s >= 0; s = xfg_table_next_slot(t, s)) {
-		if ((flags[s] & live) != live)
+		if ((flags[s] & mask) != mask)
 			continue;   /* cannot hit this lookup: as absent */
 		uint32_t k;
 		xfg_table_slot_key(t, (uint64_t)s, &k);   /* the wire bytes, as the kernel loads them */
-		const uint32_t h = xfg_qt_hash(k, seed), b = h >> rbits;
-		uint16_t *e = q->img + (uint64_t)b * XFG_QT_SLOTS;
+		const uint32_t h = xfg_qt_hash(k, q->seed), b = h >> rbits;
+		uint16_t *e = img + (uint64_t)b * XFG_QT_SLOTS;
 		const uint32_t room = homed[b] > XFG_QT_SLOTS ? XFG_QT_SLOTS - 1 : XFG_QT_SLOTS;
 		uint32_t c = 0;
 		while (c < room && (e[c] & XFG_QT_USED))
@@ -313,20 +297,57 @@ int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *fla
 			continue;
 		}
 		e[c] = (uint16_t)(XFG_QT_USED | (h & rmask));
-		q->trans[(uint64_t)b * XFG_QT_SLOTS + c] = (uint32_t)s;
+		trans[(uint64_t)b * XFG_QT_SLOTS + c] = (uint32_t)s;
 		q->placed++;
 	}
 	free(homed);
 	return 0;
 }
 
-uint32_t xfg_qt_patch(struct xfg_qt *q, uint32_t key, uint32_t slot, int add)
+int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *flags,
+		 uint32_t live, uint32_t seed)
+{
+	if (t->keylen != 4 || live < 1 || live > 3)
+		return -EINVAL;
+	const uint32_t bits = xfg_qt_bits_for(t->count);
+	const uint64_t nb = 1ull << bits, ns = nb * XFG_QT_SLOTS;
+	uint32_t nimg = 1;
+	if (live == 3)   /* one image unless some key carries exactly one direction */
+		for (int64_t s = xfg_table_next_slot(t, -1); s >= 0 && nimg == 1; s = xfg_table_next_slot(t, s))
+			if ((flags[s] & 3) == 1 || (flags[s] & 3) == 2)
+				nimg = 2;
+	if (q->bits != bits || q->nimg != nimg || !q->img) {
+		xfg_qt_free(q);
+		q->img = malloc(nimg * ns * 2);
+		q->trans = malloc(nimg * ns * 4);
+		if (!q->img || !q->trans) {
+			xfg_qt_free(q);
+			return -ENOMEM;
+		}
+	}
+	memset(q->img, 0, nimg * ns * 2);
+	memset(q->trans, 0xff, nimg * ns * 4);
+	q->bits = bits;
+	q->seed = seed;
+	q->live = live;
+	q->nimg = nimg;
+	q->nslots = (uint32_t)ns;
+	q->placed = q->spilled = 0;
+	for (uint32_t im = 0; im < nimg; im++) {
+		int err = qt_build_img(q, im, t, flags, xfg_qt_img_mask(live, nimg, im));
+		if (err)
+			return err;
+	}
+	return 0;
+}
+
+uint32_t xfg_qt_patch(struct xfg_qt *q, uint32_t im, uint32_t key, uint32_t slot, int add)
 {
 	const uint32_t rbits = 32 - q->bits, rmask = (1u << rbits) - 1;
 	const uint32_t h = xfg_qt_hash(key, q->seed), b = h >> rbits;
 	const uint16_t r = (uint16_t)(XFG_QT_USED | (h & rmask));
-	uint16_t *e = q->img + (uint64_t)b * XFG_QT_SLOTS;
-	uint32_t *tr = q->trans + (uint64_t)b * XFG_QT_SLOTS;
+	uint16_t *e = q->img + (uint64_t)im * q->nslots + (uint64_t)b * XFG_QT_SLOTS;
+	uint32_t *tr = q->trans + (uint64_t)im * q->nslots + (uint64_t)b * XFG_QT_SLOTS;
 	if (!add) {
 		for (uint32_t c = 0; c < XFG_QT_SLOTS; c++)
 			if (e[c] == r) {   /* (keys are unique: at most one entry) */

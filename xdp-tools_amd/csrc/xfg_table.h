@@ -78,14 +78,18 @@ static inline uint64_t xfg_table_img_bytes(const struct xfg_table *t)
 
 /* Quotient index of a table of 4-byte keys (layout: xfg_layout.h).  Built
  * from the table's keys and each slot's flag byte (@flags[slot], the same on
- * every device); only keys carrying mask @live are entered (the lookups it
- * answers are of that mask).  Returns 0 or
- * -ENOMEM / -EINVAL (not 4-byte keys). */
+ * every device); only keys carrying the live mask of an image's lookup are
+ * entered in it.  @live 2 (dst) or 1 (src): one image.  @live 3 (both
+ * directions): image 0 answers the dst lookup, image 1 the src lookup --
+ * unless every key with a direction bit has both (`xdp-filter ip -m
+ * src,dst` rule sets), when one image serves both lookups (nimg 1).
+ * Returns 0 or -ENOMEM / -EINVAL (not 4-byte keys). */
 struct xfg_qt {
 	uint32_t bits, seed, live;
-	uint32_t nslots;      /* (1 << bits) * XFG_QT_SLOTS */
-	uint16_t *img;        /* (1 << bits) * XFG_QT_SLOTS entries */
-	uint32_t *trans;      /* nslots: canonical slot, or ~0u */
+	uint32_t nslots;      /* per image: (1 << bits) * XFG_QT_SLOTS */
+	uint32_t nimg;        /* images: 1, or 2 (both directions, asymmetric) */
+	uint16_t *img;        /* nimg * nslots entries, image after image */
+	uint32_t *trans;      /* nimg * nslots: canonical slot, or ~0u */
 	uint32_t placed, spilled;
 };
 int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *flags,
@@ -99,7 +103,13 @@ int xfg_qt_build(struct xfg_qt *q, const struct xfg_table *t, const uint8_t *fla
  * a marked bucket only sends its misses to the canonical table, which is
  * always exact.  Returns the bucket touched.  The caller has folded the
  * QT-order counts first: an entry given to another key must count from 0. */
-uint32_t xfg_qt_patch(struct xfg_qt *q, uint32_t key, uint32_t slot, int add);
+uint32_t xfg_qt_patch(struct xfg_qt *q, uint32_t img, uint32_t key, uint32_t slot, int add);
+/* The mask a key must carry to be entered in image @img of an index of
+ * live mask @live (nimg images). */
+static inline uint32_t xfg_qt_img_mask(uint32_t live, uint32_t nimg, uint32_t img)
+{
+	return live != 3 ? live : (nimg == 1 ? 3u : (img == 0 ? 2u : 1u));
+}
 void xfg_qt_free(struct xfg_qt *q);
 /* Bucket bits for @count keys: fewer than XFG_QT_LOAD keys per 16-entry
  * bucket on average (a 1M-key map: 2^17 buckets, 4 MB). */
