@@ -396,3 +396,23 @@ def test_qt_falls_back_when_the_log_cannot_run(G):
     assert f.last_path() == 2
     assert_same(v, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
     f.close()
+
+
+@pytest.mark.parametrize("stride", [64, 128])
+def test_qt_hits_concentrated_in_few_log_partitions(G, stride):
+    """Every ruled key's index bucket is 7 or 200 mod 256, so all hits fall
+    into two hit-log partitions: the kernel's LDS rings for them fill, flush
+    in chunks, overflow into the counter cache, and end with more than a
+    wave's worth of entries each -- every count checked against the
+    restatement (xdpfilt_prog.h:56-64: one bump per hit)."""
+    rng = np.random.default_rng(81)
+    cand = rng.integers(0, 2**32, 1 << 22, dtype=np.uint64).astype(np.uint32)
+    cu8 = cand.view(np.uint8).reshape(-1, 4)
+    b = qt_bucket(cu8)
+    keys = cu8[((b & 255) == 7) | ((b & 255) == 200)][:3000]
+    keys = np.unique(keys.view("<u4").reshape(-1)).view(np.uint8).reshape(-1, 4)
+    rules = X.RuleSet()
+    rules.v4_keys = keys
+    rules.v4_vals = np.full(len(keys), 2, np.uint64)
+    data, lens = X.gen_workload(82, 3, 1 << 20, stride, v4=keys, dst_permille=700)
+    run_both(G, "xdpfilt_dny_all", rules, data, lens, stride)

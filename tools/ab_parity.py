@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--log2-packets", type=int, default=22)
     ap.add_argument("--src-dst", action="store_true", help="every rule src|dst")
+    ap.add_argument("--hot", type=int, default=0, help="every dst hit on one of N rules")
     a = ap.parse_args()
     import xfgpu as G
     n = 1 << a.log2_packets
@@ -30,7 +31,7 @@ def main():
     rules.v4_vals = np.full(len(v4), 3 if a.src_dst else 2, np.uint64)
     for p in ports:
         rules.ports[X.port_key(int(p))] = 2 | 4 | 8
-    data, lens = X.gen_workload(3, 3, n, 64, v4=v4, ports=ports)
+    data, lens = X.gen_workload(3, 3, n, 64, v4=v4[:a.hot] if a.hot else v4, ports=ports)
     if a.src_dst:   # a quarter of the IPv4 frames get a ruled source too
         d = data.reshape(-1, 64)
         ip4 = np.nonzero((d[:, 12] == 8) & (d[:, 13] == 0))[0][::4]
@@ -46,7 +47,7 @@ def main():
     st = f.stats()
     ok = (np.array_equal(v, ov) and np.array_equal(got.v4_vals, orules.v4_vals)
           and np.array_equal(got.ports, orules.ports) and np.array_equal(st, ost))
-    print(f"ab_parity lib={os.environ.get('XFG_LIB')} path={path} n={n} "
+    print(f"ab_parity lib={os.environ.get('XFG_LIB')} path={path} n={n} hot={a.hot} "
           f"verdicts={'ok' if np.array_equal(v, ov) else 'DIFF'} "
           f"v4={'ok' if np.array_equal(got.v4_vals, orules.v4_vals) else 'DIFF'} "
           f"stats={'ok' if np.array_equal(st, ost) else 'DIFF'} -> {'PASS' if ok else 'FAIL'}",

@@ -1554,21 +1554,23 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		 * most the workgroup's waves can log (a fuller one spills) */
 		uint64_t wg_max = (per_wg / 64) * (uint64_t)a.defer_cap;
 		uint64_t pcap = (2 * ((wg_max + XFG_LOG_PARTS - 1) / XFG_LOG_PARTS) + 64 + 7) & ~7ull;
-		if ((err = scratch(d, (void **)&d->tlog, &d->tlog_bytes,
-				   grid * (per_wg / 64) * (uint64_t)a.defer_cap * 4)) ||
+		/* (the quotient-index kernel combines its log in LDS and writes
+		 * the partition buffers itself: no per-wave regions) */
+		if ((!a.qt && (err = scratch(d, (void **)&d->tlog, &d->tlog_bytes,
+					     grid * (per_wg / 64) * (uint64_t)a.defer_cap * 4))) ||
 		    (err = scratch(d, (void **)&d->pbuf, &d->pbuf_bytes,
 				   ((uint64_t)XFG_LOG_PARTS * grid * pcap + 512) * 2)) ||   /* (+ the count kernel's overread) */
 		    (err = scratch(d, (void **)&d->pfill, &d->pfill_bytes,
 				   (uint64_t)XFG_LOG_PARTS * grid * 4)))
 			goto out;
-		a.tlog = d->tlog;
+		a.tlog = a.qt ? NULL : d->tlog;
 		a.pbuf = d->pbuf;
 		a.pfill = d->pfill;
 		a.pcap = (uint32_t)pcap;
 		a.pslices = (uint32_t)grid;
 		a.log_hist = (uint32_t)hist;
 	}
-	if (a.qt && !a.tlog) {   /* (decided above: cannot happen) */
+	if (a.qt && !a.pbuf) {   /* (decided above: cannot happen) */
 		err = -EIO;
 		goto out;
 	}

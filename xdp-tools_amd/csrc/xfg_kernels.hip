@@ -551,6 +551,9 @@ struct Probe {
 // Counter identity of a hit: its index in the global counter space (v4
 // slots, v6 slots, eth slots, ports; xfg_kargs.gbase), CT_NONE for none.
 constexpr uint32_t CT_NONE = 0xffffffffu;
+// (tag bit of a QT slot in the quotient-index kernel: canonical counter
+// identities stay below 2^30)
+constexpr uint32_t CT_QTAG = 0x80000000u;
 
 // Counter of global index g (threshold compares: no dynamic index into the
 // kernel-argument struct, which would put it in scratch).
@@ -826,12 +829,14 @@ struct Counters {
 				atomicAdd(global_counter(a, tag), 1ull);
 		}
 	}
-	// Workgroup end (after a barrier): LDS sums to memory.
+	// Workgroup end (after a barrier): LDS sums to memory (a tag with
+	// CT_QTAG is a QT slot: its QT-order count, xfg_pipeq_kernel).
 	__device__ __forceinline__ void flush(const xfg_kargs &a, int tid, int nthr)
 	{
 		for (int i = tid; i < CC_ENTRIES; i += nthr)
 			if (ctag[i] != CT_NONE && ccnt[i])
-				atomicAdd(global_counter(a, ctag[i]), (unsigned long long)ccnt[i]);
+				atomicAdd((ctag[i] & CT_QTAG) ? a.qt_hits + (ctag[i] & ~CT_QTAG) : global_counter(a, ctag[i]),
+					  (unsigned long long)ccnt[i]);
 		for (uint32_t i = tid; i < a.dcnt; i += nthr)
 			if (dcnt[i])
 				atomicAdd(global_counter(a, i), (unsigned long long)dcnt[i]);
@@ -1429,7 +1434,7 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128>), dim3(grid), dim3(TILE), dl, s, a);
 	}
 	hipError_t e = hipGetLastError();
-	if (e != hipSuccess || !a.tlog)
+	if (e != hipSuccess || !a.pbuf)   // (the hit log: partition buffers filled)
 		return e;
 	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS), dim3(LC_THREADS),
 			   (size_t)a.log_hist * 4, s, a, a.log_hist);

@@ -59,7 +59,10 @@ constexpr uint32_t A_DEFER = 6;
 #endif
 #define QT_WAVES(W) ((W) <= 64 ? XFG_QT_NW : 4)
 #define QT_THREADS(W) (64 * QT_WAVES(W))
-#define QT_MINW(W) ((W) <= 64 ? (2 * XFG_QT_NW + 3) / 4 : 2)
+#ifndef XFG_QT_WGCU   /* workgroups per CU the register bound assumes */
+#define XFG_QT_WGCU 2
+#endif
+#define QT_MINW(W) ((W) <= 64 ? (XFG_QT_WGCU * XFG_QT_NW + 3) / 4 : 2)
 
 // Key descriptor: kind | mask << 2 | zero << 4 | byte offset << 5.
 __device__ __forceinline__ uint32_t kd_kind(uint32_t d) { return d & 3; }

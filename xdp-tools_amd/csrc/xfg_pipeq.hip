@@ -19,11 +19,13 @@
 // no prefilter hop, no LDS.  Lanes without a lookup load bucket 0 (one
 // shared line), so they add no lines.
 //
-// Used when exactly one IPv4 lookup direction can hit (flag census), every
-// device carries the same flags, and the map is large (xfg_ctx.c
-// fill_kargs).  Results are identical to xfg_pipe4_kernel's: a miss in a
-// bucket that overflowed, and every shape the static parse does not cover,
-// go to the deferred list and the canonical table (classify_staged).
+// Used when only IPv4 keys can hit (flag census), every device carries the
+// same flags, and the map is large (xfg_ctx.c fill_kargs); with both lookup
+// directions live (BOTH) each packet reads its dst bucket and its src
+// bucket (one image for src|dst rule sets, two otherwise).  Results are
+// identical to xfg_pipe4_kernel's: a miss in a bucket that overflowed, and
+// every shape the static parse does not cover, go to the deferred list and
+// the canonical table (classify_staged).
 //
 // Per wave, iteration k works on three tiles of 64 packets:
 //   R  tile k-1's buckets (loaded by L last iteration): match -> verdict
@@ -37,33 +39,12 @@
 // One wait per iteration, at its top: everything but the newest tile's
 // CPP + 1 loads.  Every iteration issues the same loads (a lane without a
 // lookup loads bucket 0), so the count is fixed.
-#ifndef XFG_QT_EARLY_L
-#define XFG_QT_EARLY_L 1
+// The hit log is write-combined in LDS (below): ring sizes per window.
+#ifndef XFG_QT_WC_R      /* ring entries per partition, 64-byte windows */
+#define XFG_QT_WC_R 128
 #endif
-// (A/B: bucket loads as global loads (0) or buffer loads with aux XFG_QT_BKAUX;
-// window loads non-temporal (1) or plain (0))
-#ifndef XFG_QT_BKPOL
-#define XFG_QT_BKPOL 0
-#endif
-#ifndef XFG_QT_BKAUX
-#define XFG_QT_BKAUX 0
-#endif
-#ifndef XFG_QT_WIN_NT
-#define XFG_QT_WIN_NT 1
-#endif
-// (A/B: verdict bytes packed four to a dword store (1) or a byte per lane (0);
-// non-temporal (1) or plain (0))
-#ifndef XFG_QT_VPACK
-#define XFG_QT_VPACK 0
-#endif
-// (A/B: tile k-1's verdict and hit-log stores issued last in the iteration,
-// after tile k+2's loads, as a fixed two instructions -- so that the next
-// iteration's one wait does not wait for their write acknowledgements)
-#ifndef XFG_QT_LATE
-#define XFG_QT_LATE 0
-#endif
-#ifndef XFG_QT_VNT
-#define XFG_QT_VNT 1
+#ifndef XFG_QT_WC_R128   /* ... 128-byte windows (4 waves: two workgroups a CU) */
+#define XFG_QT_WC_R128 32
 #endif
 
 namespace {
@@ -71,7 +52,6 @@ namespace {
 template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH>
 __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
-	static_assert(!BOTH || XFG_QT_EARLY_L, "both directions: the keys are hashed before the parse");
 	static_assert((FEAT & F_IPV4) != 0, "IPv4-key mode needs the IPv4 feature");
 	constexpr int NW = QT_WAVES(W);
 	constexpr int NT = 64 * NW;
@@ -80,8 +60,25 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
-	constexpr uint32_t QTAG = 0x80000000u;   // tag bit: a QT slot (hit log), not a counter identity
-	__shared__ uint32_t win[NW * 64 * ROWDW > LOG_SCRATCH ? NW * 64 * ROWDW : LOG_SCRATCH];
+	constexpr uint32_t QTAG = CT_QTAG;   // tag bit: a QT slot (hit log), not a counter identity
+	// Write-combined hit log.  A QT hit of partition p = log_part(slot)
+	// goes, as its 16-bit local index, into p's ring of WR entries in LDS
+	// (reserve a place: s_res[p]; take a ticket: s_hd[2p]; write; count the
+	// write done: s_hd[2p + 1]).  Wave p % NW owns p: once an iteration it
+	// moves completed chunks of WF entries (all tickets written: done ==
+	// head) into the workgroup's slice of p's partition buffer -- the
+	// layout log_partition writes and xfg_log_count_kernel reads -- and
+	// gives their places back.  A hit that finds the ring full (a hot key)
+	// is summed in the LDS counter cache instead (QT tag), as is a chunk
+	// that would overrun the slice.  No per-wave log, no workgroup-end sort.
+	constexpr uint32_t PPW = XFG_LOG_PARTS / NW;   // partitions a wave owns: lane * NW + wave
+	static_assert(PPW * NW == XFG_LOG_PARTS && PPW <= 64, "partition ownership");
+	constexpr uint32_t WR = W <= 64 ? XFG_QT_WC_R : XFG_QT_WC_R128, WF = WR / 2;
+	static_assert((WR & (WR - 1)) == 0 && WF <= 64, "ring: a power of two");
+	__shared__ uint32_t win[NW * 64 * ROWDW];
+	__shared__ uint16_t s_ring[XFG_LOG_PARTS * WR];
+	__shared__ uint32_t s_res[XFG_LOG_PARTS];
+	__shared__ __attribute__((aligned(8))) uint32_t s_hd[2 * XFG_LOG_PARTS];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
 	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB : 1];
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
@@ -109,11 +106,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// (both directions: the src lookup's image and its QT slots' offset)
 	const uint64_t qb2 = BOTH ? rfl64((uint64_t)(uintptr_t)a.qt2) : 0;
 	const uint32_t qbase2 = BOTH ? rfl(a.qt_base) : 0u;
-#if XFG_QT_BKPOL != 0
-	// (A/B: the bucket loads as buffer loads with cache policy XFG_QT_BKAUX)
-	const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
-		(void *)a.qt, 0, (int)((64ull << qbits) < 0x7fffffffull ? (64ull << qbits) : 0x7fffffffull), 0x00020000);
-#endif
 	const bool klive = a.t4.count != 0;
 	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
 	cn.init(a, tid, NT);
@@ -127,6 +119,16 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			s_pcnt[i] = 0;
 	for (int i = tid; i < (int)XFG_LOG_PARTS; i += NT)
 		s_lh[i] = 0;
+	for (int i = tid; i < (int)XFG_LOG_PARTS; i += NT) {
+		s_res[i] = 0;
+		s_hd[2 * i] = 0;
+		s_hd[2 * i + 1] = 0;
+	}
+	// this lane's partition (lanes below PPW), the entries it has moved out
+	const uint32_t wc_p = (uint32_t)lane * NW + (uint32_t)wv;
+	uint32_t wc_fl = 0;
+	const uint64_t wc_slice0 = (uint64_t)blockIdx.x * a.pcap;
+	const uint64_t wc_pstep = (uint64_t)a.pslices * a.pcap;
 	__syncthreads();
 
 	uint32_t *const rows = win + wv * 64 * ROWDW;
@@ -148,10 +150,19 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			if (q)
 				atomicAdd(reinterpret_cast<uint32_t *>(a.pbuf) + qs, 1u);
 		} else {
-			if (!(dg & 16384))   // (diagnostics: no hit-log store)
-				log_append(tregion, tn, pick(q, qs, CT_NONE), lane);
-			if (q)
-				atomicAdd(&s_lh[log_part(qs)], 1u);
+			if (q) {
+				const uint32_t p = log_part(qs);
+				const uint32_t r = atomicAdd(&s_res[p], 1u);
+				if (r < WR) {
+					const uint32_t t = atomicAdd(&s_hd[2 * p], 1u);
+					s_ring[p * WR + (t & (WR - 1))] = (uint16_t)log_local(qs);
+					atomicAdd(&s_hd[2 * p + 1], 1u);
+				} else {   // the ring is full: the LDS counter cache
+					atomicSub(&s_res[p], 1u);
+					if (!cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
+						atomicAdd(a.qt_hits + qs, 1ull);
+				}
+			}
 		}
 		if constexpr (PORTS)
 			if (ps)
@@ -159,6 +170,44 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		if (dc & !ps)
 			atomicAdd(&cn.dcnt[tag], 1u);
 		cn.bump(a, pick(q | dc | ps, CT_NONE, tag), lane);
+	};
+	// move entries [fl, fl + cnt) of lane j's partition to its slice (cnt
+	// <= WR; positions past pcap: the counter cache instead)
+	auto wc_move = [&](uint32_t j, uint32_t fl, uint32_t cnt) {
+		const uint32_t p = j * NW + (uint32_t)wv;
+		for (uint32_t o = lane; o < cnt; o += 64) {
+			const uint32_t e = s_ring[p * WR + ((fl + o) & (WR - 1))];
+			const uint32_t pos = fl + o;
+			if (pos < a.pcap)
+				*reinterpret_cast<__attribute__((address_space(1))) uint16_t *>(
+					(uintptr_t)(a.pbuf + p * wc_pstep + wc_slice0 + pos)) = (uint16_t)e;
+			else {
+				const uint32_t g = ((e >> 4) << 12) | (p << 4) | (e & 15);
+				if (!cache_hit(cn.ctag, cn.ccnt, QTAG | g, 1))
+					atomicAdd(a.qt_hits + g, 1ull);
+			}
+		}
+	};
+	// once an iteration: this wave's partitions' completed chunks
+	auto wc_flush = [&]() {
+		// head and done of the partition in ONE 8-byte read (a snapshot):
+		// done == head means every ticket taken has been written
+		uint32_t hd0 = 0, hd1 = 0;
+		if ((uint32_t)lane < PPW) {
+			const uint64_t v = *reinterpret_cast<const uint64_t *>(&s_hd[2 * wc_p]);
+			hd0 = (uint32_t)v;
+			hd1 = (uint32_t)(v >> 32);
+		}
+		unsigned long long fm = __ballot(((uint32_t)lane < PPW) & (hd0 == hd1) & (hd1 - wc_fl >= WF));
+		while (fm) {
+			const uint32_t j = (uint32_t)__ffsll((long long)fm) - 1;
+			fm &= fm - 1;
+			const uint32_t fl = __builtin_amdgcn_readlane(wc_fl, j);
+			wc_move(j, fl, WF);
+			if (lane == 0)   // (after the ring reads: LDS keeps a wave's order)
+				atomicSub(&s_res[j * NW + wv], WF);
+			wc_fl += (uint32_t)lane == j ? WF : 0u;
+		}
 	};
 	const uint32_t n = (uint32_t)a.n;
 	const uint32_t nt = (n + 63) / 64;
@@ -174,9 +223,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		st_b2 += pick(act == A_PASS, len, 0u);
 	};
 	uint32_t ndef = 0;
-#if XFG_QT_VPACK
-	const bool vpk = ((uintptr_t)a.verdicts & 3) == 0;
-#endif
 
 	// windows + lengths of tile t (clamped to the last tile): CPP + 1 loads,
 	// always issued
@@ -199,11 +245,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
 				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
 							 : reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
-#if XFG_QT_WIN_NT
 				pre[it] = __builtin_nontemporal_load(src);
-#else
-				pre[it] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>((uintptr_t)src);
-#endif
 			}
 			plen = *reinterpret_cast<const __attribute__((address_space(1))) len_t *>(
 				lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
@@ -230,8 +272,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	uint32_t r_key = 0, r_b = 0, r_pk = pk3(A_NONE, XFG_PORT_TAB, 0), r_tag = CT_NONE;
 	bool r_sel = false;
 	u32x4 bk0 = { 0, 0, 0, 0 }, bk1 = { 0, 0, 0, 0 };
-	// (both directions: the src key's entry, bucket and bucket halves)
+	// (both directions: the src key's entry and bucket from P; tile k-1's
+	// state after its dst lookup, for R2 next iteration; its src bucket)
 	uint32_t r_key2 = 0, r_b2 = 0;
+	bool q_need = false;
+	uint32_t q_act = A_NONE, q_tag = CT_NONE, q_ps = XFG_PORT_TAB, q_len = 0, q_key2 = 0, q_b2 = 0;
 	u32x4 bs0 = { 0, 0, 0, 0 }, bs1 = { 0, 0, 0, 0 };
 	// one bucket's 16 entries (halves in lanes i and i + 32 of h0 / h1, see
 	// L) searched for entry q: found, its index, the overflow marker
@@ -254,24 +299,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 		return (w[7] >> 16) == XFG_QT_OVF_MARK;
 	};
-#if XFG_QT_LATE
-	// the late stores' lanes: verdict address / byte, log position / entry
-	uint32_t ls_gi = 0, ls_act = 0, ls_pos = 0, ls_val = 0;
-	// (iteration 0 -- the only one without a tile to resolve -- is peeled:
-	// every later one resolves a tile and ends with exactly two stores, so
-	// the wait that ends an iteration has a fixed count)
-	auto iteration = [&](auto peel_c, uint32_t k, u32x4 (&cur)[CPP], len_t &curlen) {
-		constexpr bool PEEL = decltype(peel_c)::value;
-		const uint32_t tP = first + k * step;
-		const bool vP = tP < nt;
-		constexpr bool vR = !PEEL;   // (k >= 1: tile first + (k-1) step < nt)
-#else
 	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen) {
 		const uint32_t tP = first + k * step;
 		const bool vP = tP < nt;
 		const bool vR = k >= 1 && tP - step < nt;
 		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
-#endif
 		// (the length is used from here on: without this the compiler
 		// rotates its zero-extension to the previous iteration's end, where
 		// it waits for the load -- and every older one -- early)
@@ -279,8 +311,32 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 
 		PMARK("R");
 		// ---- R: tile k-1's bucket -> CHECK_MAP (xdpfilt_prog.h:56-64)
-		const uint32_t r_act = pk_act(r_pk), r_ps = pk_ps(r_pk), w_len = pk_len(r_pk);
-		uint32_t w_act = A_NONE, w_tag = CT_NONE, w_ps = r_ps;
+		const uint32_t r_act = pk_act(r_pk), r_ps = pk_ps(r_pk), r_len = pk_len(r_pk);
+		uint32_t w_act = A_NONE, w_tag = CT_NONE, w_ps = r_ps, w_len = r_len;
+		// (both directions: W works on tile k-2, whose src lookup -- read
+		// last iteration for the packets whose dst lookup decided nothing --
+		// R2 resolves first; one directions: W works on tile k-1)
+		const bool vW = BOTH ? (k >= 2 && tP - 2 * step < nt) : vR;
+		if constexpr (BOTH) {
+			PMARK("R2");
+			// lookup_verdict_ipv4 (xdpfilt_prog.h:121-134): the src key
+			// only when the dst key decided nothing -- the first matching
+			// lookup's counter alone is bumped
+			w_act = q_act;
+			w_tag = q_tag;
+			w_ps = q_ps;
+			w_len = q_len;
+			if (vW && !(dg & 8192)) {
+				bool f2;
+				uint32_t ix2;
+				const bool ovf2 = match(bs0, bs1, q_key2, f2, ix2);
+				f2 &= q_need;
+				const bool d2 = q_need & !f2 & ovf2;
+				w_act = pick(f2, HIT, pick(d2, A_DEFER, w_act));
+				w_tag = pick(f2, QTAG | (qbase2 + q_b2 * XFG_QT_SLOTS + ix2), pick(d2, CT_NONE, w_tag));
+				w_ps = pick(f2 | d2, XFG_PORT_TAB, w_ps);
+			}
+		}
 		if (vR && !(dg & 8192)) {
 			// 16 entries, filled in order; keys are unique, so at most one
 			// matches.  A miss in a bucket marked overflowed may be a key
@@ -292,102 +348,49 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			uint32_t ix;
 			const bool ovf = match(bk0, bk1, r_key, found, ix);
 			found &= r_sel;
-			bool defer = r_sel & !found & ovf;
-			uint32_t slot = r_b * XFG_QT_SLOTS + ix;
-			if constexpr (BOTH) {
-				// lookup_verdict_ipv4 (xdpfilt_prog.h:121-134): the src
-				// key only when the dst key decided nothing -- the first
-				// matching lookup's counter alone is bumped
-				bool f2;
-				uint32_t ix2;
-				const bool ovf2 = match(bs0, bs1, r_key2, f2, ix2);
-				const bool open = r_sel & !found & !defer;
-				f2 &= open;
-				defer |= open & !f2 & ovf2;
-				slot = pick(f2, qbase2 + r_b2 * XFG_QT_SLOTS + ix2, slot);
-				found |= f2;
+			const bool defer = r_sel & !found & ovf;
+			const uint32_t slot = r_b * XFG_QT_SLOTS + ix;
+			const uint32_t x_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
+			const uint32_t x_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, r_tag));
+			const uint32_t x_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
+			if constexpr (BOTH) {   // to R2 next iteration
+				q_need = r_sel & !found & !defer;
+				q_act = x_act;
+				q_tag = x_tag;
+				q_ps = x_ps;
+				q_len = r_len;
+				q_key2 = r_key2;
+				q_b2 = pick(q_need, r_b2, 0u);
+			} else {
+				w_act = x_act;
+				w_tag = x_tag;
+				w_ps = x_ps;
 			}
-			w_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
-			w_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, r_tag));
-			w_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
+		} else if constexpr (BOTH) {
+			q_need = false;
+			q_act = A_NONE;
+			q_tag = CT_NONE;
+			q_ps = XFG_PORT_TAB;
+			q_b2 = 0;
+		}
+		if constexpr (BOTH) {
+			// tile k-1's src buckets (bucket 0 for a packet whose dst lookup
+			// decided it: a shared line), as L loads (see there)
+			if (!(dg & 2)) {
+				const auto ab2 = __builtin_amdgcn_permlane32_swap(q_b2, q_b2, false, false);
+				const uint64_t hb2 = qb2 + (uint64_t)(lane >> 5) * 16;
+				bs0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[0] << 5));
+				bs1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[1] << 5));
+			}
 		}
 
 		PMARK("W");
-		// ---- W: verdicts, counters, stats, deferrals of tile k-1
-#if XFG_QT_LATE
-		if (vR) {
-			const uint32_t tb = (tP - step) * 64, gi = tb + lane;
-			// verdict: every lane stores (a fixed instruction): a deferred
-			// lane a placeholder the deferred pass overwrites, a lane past
-			// the batch's end lane 0's byte at lane 0's address
-			const uint32_t a0 = __builtin_amdgcn_readfirstlane(w_act);
-			ls_gi = pick(gi < n, gi, tb);
-			ls_act = pick(gi < n, w_act, a0);
-			// hit log: a block of 64 entries at tn, the hits first, then
-			// CT_NONE padding the next block overwrites (the count advances
-			// by the hits only; a wave's region has room: tn + 64 <= its
-			// packets so far + 64 <= defer_cap)
-			const bool q = (w_tag != CT_NONE) & ((w_tag & QTAG) != 0) & !(dg & 1);
-			const unsigned long long m = __ballot(q);
-			ls_pos = tn + pick(q, lanes_below(m), (uint32_t)__popcll(m) + lanes_below(~m));
-			ls_val = pick(q, w_tag & ~QTAG, CT_NONE);
-			tn += (uint32_t)__popcll(m);
-			if (q)
-				atomicAdd(&s_lh[log_part(w_tag & ~QTAG)], 1u);
-			const uint32_t ctag = (dg & 1) ? CT_NONE : pick(q, CT_NONE, w_tag);
-			const uint32_t cps = (dg & 1) ? XFG_PORT_TAB : w_ps;
-			if constexpr (PORTS)
-				if (cps < XFG_PORT_TAB)
-					atomicAdd(&s_pcnt[cps], 1u);
-			const bool dc = (ctag != CT_NONE) & (ctag < a.dcnt) & !(cps < XFG_PORT_TAB);
-			if (dc)
-				atomicAdd(&cn.dcnt[ctag], 1u);
-			cn.bump(a, pick(dc | (cps < XFG_PORT_TAB), CT_NONE, ctag), lane);
-			if (!(dg & 128))
-				stat(w_act, w_len);
-			const unsigned long long dm = (dg & 128) ? 0ull : __ballot(w_act == A_DEFER);
-			if (dm) {
-				const uint32_t pos = ndef + lanes_below(dm);
-				if (w_act == A_DEFER)
-					gst32(dlist + pos, gi);
-				ndef += (uint32_t)__popcll(dm);
-			}
-		}
-#else
-		if (vR) {
-			const uint32_t gi = (tP - step) * 64 + lane;
-#if XFG_QT_VPACK
-			// a whole tile's 64 verdict bytes as 16 dwords (lanes 4j, the
-			// bytes of lanes 4j..4j+3 gathered by DPP): a deferred lane's
-			// byte is a placeholder the deferred pass overwrites
-			if (!(dg & 8)) {
-				const uint32_t tb = (tP - step) * 64;
-				if (vpk & (n - tb >= 64)) {
-					const uint32_t b = w_act & 0xffu;
-					const uint32_t x = b | ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 249, 0xf, 0xf, false) << 8) |
-							   ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 254, 0xf, 0xf, false) << 16) |
-							   ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 255, 0xf, 0xf, false) << 24);
-					if ((lane & 3) == 0) {
-						auto *vp = reinterpret_cast<__attribute__((address_space(1))) uint32_t *>(
-							(uintptr_t)(a.verdicts + gi));
-#if XFG_QT_VNT
-						__builtin_nontemporal_store(x, vp);
-#else
-						*vp = x;
-#endif
-					}
-				} else if (w_act <= A_PASS)
-					__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
-			}
-#else
+		// ---- W: verdicts, counters, stats, deferrals of tile k-1 (k-2)
+		if (vW) {
+			const uint32_t gi = (tP - (BOTH ? 2 : 1) * step) * 64 + lane;
 			if (w_act <= A_PASS && !(dg & 8)) {
-#if XFG_QT_VNT
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
-#else
-				*reinterpret_cast<__attribute__((address_space(1))) uint8_t *>((uintptr_t)(a.verdicts + gi)) = (uint8_t)w_act;
-#endif
 			}
-#endif
 			count((dg & 1) ? CT_NONE : w_tag, (dg & 1) ? XFG_PORT_TAB : w_ps);
 			if (!(dg & 128))
 				stat(w_act, w_len);
@@ -399,7 +402,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
-#endif
+		if (vW)
+			wc_flush();
 
 		PMARK("S");
 		// ---- S: tile k's windows into the rows, lengths clamped to the
@@ -430,7 +434,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			__builtin_amdgcn_wave_barrier();
 		}
 
-#if XFG_QT_EARLY_L
 		PMARK("L");
 		// ---- K + L: the key's hash from the row's fixed dwords and tile
 		// k's bucket loads first, the rest of the parse after them (the
@@ -440,43 +443,22 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// looked up once); R moves them to the packet's lane.  Every lane
 		// loads (a fixed count); one whose frame is not IPv4 loads bucket 0
 		// (a shared line).
-		uint32_t hk = 0, lbk = 0, hk2 = 0, lbk2 = 0;
+		uint32_t hk = 0, lbk = 0, hk2 = 0;
 		if (vP) {
 			const uint32_t e3 = myrow[3], e6 = myrow[6], e7 = myrow[7], e8 = myrow[8];
 			const uint32_t key = dlive ? __builtin_amdgcn_alignbyte(e8, e7, 2) : __builtin_amdgcn_alignbyte(e7, e6, 2);
 			hk = xfg_qt_hash(key, qseed);
 			lbk = pick((e3 & 0xffffu) == 0x0008u, hk >> rsh, 0u);
-			if constexpr (BOTH) {   // the src key (saddr, bytes 26..29)
+			if constexpr (BOTH)   // the src key (saddr, bytes 26..29)
 				hk2 = xfg_qt_hash(__builtin_amdgcn_alignbyte(e7, e6, 2), qseed);
-				lbk2 = pick((e3 & 0xffffu) == 0x0008u, hk2 >> rsh, 0u);
-			}
 		}
 		if (!(dg & 2)) {
 			const auto ab = __builtin_amdgcn_permlane32_swap(lbk, lbk, false, false);
-#if XFG_QT_BKPOL == 0
 			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
 			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
 			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
-			if constexpr (BOTH) {
-				const auto ab2 = __builtin_amdgcn_permlane32_swap(lbk2, lbk2, false, false);
-				const uint64_t hb2 = qb2 + (uint64_t)(lane >> 5) * 16;
-				bs0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[0] << 5));
-				bs1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[1] << 5));
-			}
-#else
-			const uint32_t ho = (uint32_t)(lane >> 5) * 16;
-			bk0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ho + (ab[0] << 5), 0, XFG_QT_BKAUX);
-			bk1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ho + (ab[1] << 5), 0, XFG_QT_BKAUX);
-			if constexpr (BOTH) {
-				const auto ab2 = __builtin_amdgcn_permlane32_swap(lbk2, lbk2, false, false);
-				const uint32_t ob = qbase2 * 2;   // (image 1's byte offset: 0 with one image)
-				bs0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ob + ho + (ab2[0] << 5), 0, XFG_QT_BKAUX);
-				bs1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, ob + ho + (ab2[1] << 5), 0, XFG_QT_BKAUX);
-			}
-#endif
 		}
 		__builtin_amdgcn_sched_barrier(0);
-#endif
 		PMARK("P");
 		// ---- P: parse tile k, hash its key, plan its fallback
 		if (vP && (dg & 64)) {   // (diagnostics: no parse)
@@ -491,12 +473,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
 			const bool kok = valid & !r.defer & r.v4ok & klive;
-#if XFG_QT_EARLY_L
 			const uint32_t h = hk;
-#else
-			const uint32_t key = dlive ? r.k4a : r.k4b;
-			const uint32_t h = xfg_qt_hash(key, qseed);
-#endif
 			r_b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
 			r_key = XFG_QT_USED | (h & rmask);
 			r_sel = kok;
@@ -540,20 +517,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			r_tag = CT_NONE;
 		}
 
-#if !XFG_QT_EARLY_L
-		PMARK("L");
-		// ---- L: tile k's buckets: load q carries packets 32q..32q+31, lane
-		// L the 16-byte half L >> 5 of packet 32q + (L & 31)'s bucket, so
-		// both halves of a bucket are in ONE instruction (a line is looked
-		// up once); R moves them to the packet's lane.  Every lane loads
-		// (a fixed count).
-		if (!(dg & 2)) {
-			const auto ab = __builtin_amdgcn_permlane32_swap(r_b, r_b, false, false);
-			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
-			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
-			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
-		}
-#endif
 		PMARK("I");
 		// ---- tile k+2's windows, last: in flight for two iterations
 		// (issued before the parse instead, the compiler's register
@@ -561,19 +524,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		__builtin_amdgcn_sched_barrier(0);
 		issue(tP + 2 * step, cur, curlen);
 		__builtin_amdgcn_sched_barrier(0);
-#if XFG_QT_LATE
-		if constexpr (!PEEL) {
-			__builtin_nontemporal_store((uint8_t)ls_act,
-				reinterpret_cast<__attribute__((address_space(1))) uint8_t *>((uintptr_t)(a.verdicts + ls_gi)));
-			gst32(tregion + ls_pos, ls_val);
-			__builtin_amdgcn_sched_barrier(0);
-			// the next iteration's data: everything but tile k+2's loads
-			// and these two stores
-			__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 3) & 15) | (((CPP + 3) >> 4) << 14));
-		} else {
-			__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
-		}
-#endif
 	};
 
 	u32x4 preA[CPP], preB[CPP];
@@ -584,20 +534,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		issue(first + step, preB, lenB);
 		__builtin_amdgcn_sched_barrier(0);
 	}
-	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 2 : 0u;
-#if XFG_QT_LATE
-	if (iters) {   // (iters >= 2 whenever the wave has a tile)
-		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
-		iteration(std::true_type{}, 0, preA, lenA);
-		uint32_t k = 1;
-		for (; k + 1 < iters; k += 2) {
-			iteration(std::false_type{}, k, preB, lenB);
-			iteration(std::false_type{}, k + 1, preA, lenA);
-		}
-		if (k < iters)
-			iteration(std::false_type{}, k, preB, lenB);
-	}
-#else
+	// (one more with both directions: the last tile's src lookup resolves
+	// an iteration after its dst lookup)
+	const uint32_t iters = first < nt ? (nt - 1 - first) / step + (BOTH ? 3 : 2) : 0u;
 	uint32_t k = 0;
 	for (; k + 1 < iters; k += 2) {
 		iteration(k, preA, lenA);
@@ -605,14 +544,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	}
 	if (k < iters)
 		iteration(k, preA, lenA);
-#endif
 
 	if (dg & 2048)
 		ndef = 0;
-#if XFG_QT_VPACK || XFG_QT_LATE
-	if (ndef)   // (the placeholder bytes of the packed / late stores land first)
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
 	// the deferred packets: the whole reference walk over the canonical
 	// table (classify_staged), 64 at a time
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
@@ -643,6 +577,20 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	if (lane == 0)
 		s_tn[wv] = tn;
 	__syncthreads();
+	// (every wave's appends are done: done == head) the rest of this
+	// wave's partitions, and the slices' fills for the count kernel; a
+	// position past a slice goes to the counter cache, flushed below
+	if (a.pbuf && !(dg & 16)) {
+		const uint32_t hd = (uint32_t)lane < PPW ? s_hd[2 * wc_p] : 0u;
+		for (uint32_t j = 0; j < PPW; j++) {
+			const uint32_t fl = __builtin_amdgcn_readlane(wc_fl, j);
+			const uint32_t h = __builtin_amdgcn_readlane(hd, j);
+			wc_move(j, fl, h - fl);
+		}
+		if ((uint32_t)lane < PPW)
+			gst32(a.pfill + (uint64_t)wc_p * a.pslices + blockIdx.x, hd);
+	}
+	__syncthreads();
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
 	cn.flush(a, tid, NT);
@@ -653,8 +601,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
 	if (dg & 16)
 		return;
-	if (a.tlog)   // (win is free now: the partition scratch)
-		log_partition<NW>(a, s_tn, s_lh, win, tid);
 }
 
 }  // namespace
