@@ -28,6 +28,7 @@
 #include "xfg_table.h"
 
 /* from xfg_kernels.hip */
+int xfg_launch_log_count(const struct xfg_kargs *a, void *stream);
 int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a, unsigned grid,
 			void *stream);
 int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sink, unsigned grid,
@@ -438,6 +439,7 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	d->last_kind = -1;
 	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
+
 	for (int k = 0; k < 6; k++)
 		for (int w = 0; w < 2; w++)
 			for (int c = 0; c < 4; c++)
@@ -1581,8 +1583,15 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	}
 	if (a.qt_hits && iters > 0)
 		d->qt_pending = 1;
-	for (int i = 0; i < iters && !err; i++)
+	/* classify, then its hit log's count kernel, on the device stream (a
+	 * count kernel on a second stream, overlapped with the next classify,
+	 * shares the CUs and slowed the classify more than it hid:
+	 * profiles/r04_s11_count_overlap.log) */
+	for (int i = 0; i < iters && !err; i++) {
 		err = xfg_launch_classify(ctx->prog_features, &a, (unsigned)grid, d->stream);
+		if (!err)
+			err = xfg_launch_log_count(&a, d->stream);
+	}
 	if (!err)
 		d->last_kind = kind;
 	if (!err && user && user != (void *)d->stream) {

@@ -1433,11 +1433,6 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 	} else {
 		hipLaunchKernelGGL((xfg_classify_kernel<FEAT, 128>), dim3(grid), dim3(TILE), dl, s, a);
 	}
-	hipError_t e = hipGetLastError();
-	if (e != hipSuccess || !a.pbuf)   // (the hit log: partition buffers filled)
-		return e;
-	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS), dim3(LC_THREADS),
-			   (size_t)a.log_hist * 4, s, a, a.log_hist);
 	return hipGetLastError();
 }
 
@@ -1446,6 +1441,17 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 // Feature words of the ten programs (xdp-filter/xdpfilt_*.c + :313-315).
 #define XFG_ALL (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH)
 #define XFG_ALLOW (1u << 5)
+
+// The hit log's count kernel (after a classify that filled a.pbuf / a.pfill;
+// the host may run it on a second stream, overlapped with the next classify)
+extern "C" int xfg_launch_log_count(const struct xfg_kargs *a, void *stream)
+{
+	if (!a->pbuf)
+		return 0;
+	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS), dim3(LC_THREADS),
+			   (size_t)a->log_hist * 4, static_cast<hipStream_t>(stream), *a, a->log_hist);
+	return hipGetLastError() == hipSuccess ? 0 : -(int)hipGetLastError() - 1000;
+}
 
 extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a,
 				   unsigned grid, void *stream)

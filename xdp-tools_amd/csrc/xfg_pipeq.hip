@@ -43,6 +43,9 @@
 #ifndef XFG_QT_WC_R      /* ring entries per partition, 64-byte windows */
 #define XFG_QT_WC_R 128
 #endif
+#ifndef XFG_QT_WC_F      /* flush chunk, 64-byte windows: 64 entries, one 128-byte line */
+#define XFG_QT_WC_F 64
+#endif
 #ifndef XFG_QT_WC_R128   /* ... 128-byte windows (4 waves: two workgroups a CU) */
 #define XFG_QT_WC_R128 32
 #endif
@@ -73,7 +76,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// that would overrun the slice.  No per-wave log, no workgroup-end sort.
 	constexpr uint32_t PPW = XFG_LOG_PARTS / NW;   // partitions a wave owns: lane * NW + wave
 	static_assert(PPW * NW == XFG_LOG_PARTS && PPW <= 64, "partition ownership");
-	constexpr uint32_t WR = W <= 64 ? XFG_QT_WC_R : XFG_QT_WC_R128, WF = WR / 2;
+	constexpr uint32_t WR = W <= 64 ? XFG_QT_WC_R : XFG_QT_WC_R128;
+	constexpr uint32_t WF = W <= 64 ? XFG_QT_WC_F : WR / 2;   // flush chunk
 	static_assert((WR & (WR - 1)) == 0 && WF <= 64, "ring: a power of two");
 	__shared__ uint32_t win[NW * 64 * ROWDW];
 	__shared__ uint16_t s_ring[XFG_LOG_PARTS * WR];
@@ -135,8 +139,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const uint32_t *const myrow = rows + lane * ROWDW;
 	uint32_t *const dlist = reinterpret_cast<uint32_t *>(
 		rfl64((uint64_t)(uintptr_t)(a.defer + ((uint64_t)blockIdx.x * NW + wv) * a.defer_cap)));
-	uint32_t *const tregion = reinterpret_cast<uint32_t *>(
-		rfl64((uint64_t)(uintptr_t)(a.tlog + ((uint64_t)blockIdx.x * NW + wv) * a.defer_cap)));
 	uint32_t tn = 0;
 	// a hit's counter: a QT slot to the hit log (the host runs this kernel
 	// only with the log on); a ruled port's to its table slot's LDS
