@@ -60,7 +60,7 @@ constexpr uint32_t A_DEFER = 6;
 #define QT_WAVES(W) ((W) <= 64 ? XFG_QT_NW : 4)
 #define QT_THREADS(W) (64 * QT_WAVES(W))
 #ifndef XFG_QT_WGCU   /* workgroups per CU the register bound assumes */
-#define XFG_QT_WGCU 2
+#define XFG_QT_WGCU 1
 #endif
 #define QT_MINW(W) ((W) <= 64 ? (XFG_QT_WGCU * XFG_QT_NW + 3) / 4 : 2)
 

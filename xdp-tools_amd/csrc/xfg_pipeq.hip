@@ -40,6 +40,9 @@
 // CPP + 1 loads.  Every iteration issues the same loads (a lane without a
 // lookup loads bucket 0), so the count is fixed.
 // The hit log is write-combined in LDS (below): ring sizes per window.
+#ifndef XFG_QT_LAG       /* iterations between a tile's bucket loads and their match */
+#define XFG_QT_LAG 1
+#endif
 #ifndef XFG_QT_WC_R      /* ring entries per partition, 64-byte windows */
 #define XFG_QT_WC_R 128
 #endif
@@ -62,6 +65,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr int ROWDW = W / 4 + 1;
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
+	constexpr uint32_t LAG = XFG_QT_LAG;
+	static_assert(LAG == 1 || LAG == 2, "bucket lag: one or two iterations");
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	constexpr uint32_t QTAG = CT_QTAG;   // tag bit: a QT slot (hit log), not a counter identity
 	// Write-combined hit log.  A QT hit of partition p = log_part(slot)
@@ -271,12 +276,17 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	auto pk_len = [](uint32_t p) { return p >> 15; };
 	// P -> R (tile k-1): entry to find (USED | remainder), bucket, its
 	// 32 bytes (L -> R), fallback
-	uint32_t r_key = 0, r_b = 0, r_pk = pk3(A_NONE, XFG_PORT_TAB, 0), r_tag = CT_NONE;
-	bool r_sel = false;
-	u32x4 bk0 = { 0, 0, 0, 0 }, bk1 = { 0, 0, 0, 0 };
+	// (XFG_QT_LAG 2: a tile's buckets are matched two iterations after its
+	// loads, in the state set of its iteration's parity)
+	struct RSt {
+		uint32_t key, b, pk, tag, key2, b2;
+		bool sel;
+		u32x4 bk0, bk1;
+	};
+	RSt stA = { 0, 0, pk3(A_NONE, XFG_PORT_TAB, 0), CT_NONE, 0, 0, false, { 0, 0, 0, 0 }, { 0, 0, 0, 0 } };
+	RSt stB = stA;
 	// (both directions: the src key's entry and bucket from P; tile k-1's
 	// state after its dst lookup, for R2 next iteration; its src bucket)
-	uint32_t r_key2 = 0, r_b2 = 0;
 	bool q_need = false;
 	uint32_t q_act = A_NONE, q_tag = CT_NONE, q_ps = XFG_PORT_TAB, q_len = 0, q_key2 = 0, q_b2 = 0;
 	u32x4 bs0 = { 0, 0, 0, 0 }, bs1 = { 0, 0, 0, 0 };
@@ -301,11 +311,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 		return (w[7] >> 16) == XFG_QT_OVF_MARK;
 	};
-	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen) {
+	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen, RSt &rs) {
 		const uint32_t tP = first + k * step;
 		const bool vP = tP < nt;
-		const bool vR = k >= 1 && tP - step < nt;
-		__builtin_amdgcn_s_waitcnt(0x0F70 | ((CPP + 1) & 15) | (((CPP + 1) >> 4) << 14));
+		const bool vR = k >= LAG && tP - LAG * step < nt;
+		// everything but the newest iteration's loads (LAG 1: tile k+1's
+		// windows; LAG 2: also the last iteration's bucket loads)
+		constexpr uint32_t VW = CPP + 1 + (LAG - 1) * 2;
+		__builtin_amdgcn_s_waitcnt(0x0F70 | (VW & 15) | ((VW >> 4) << 14));
 		// (the length is used from here on: without this the compiler
 		// rotates its zero-extension to the previous iteration's end, where
 		// it waits for the load -- and every older one -- early)
@@ -313,12 +326,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 
 		PMARK("R");
 		// ---- R: tile k-1's bucket -> CHECK_MAP (xdpfilt_prog.h:56-64)
-		const uint32_t r_act = pk_act(r_pk), r_ps = pk_ps(r_pk), r_len = pk_len(r_pk);
+		const uint32_t r_act = pk_act(rs.pk), r_ps = pk_ps(rs.pk), r_len = pk_len(rs.pk);
 		uint32_t w_act = A_NONE, w_tag = CT_NONE, w_ps = r_ps, w_len = r_len;
 		// (both directions: W works on tile k-2, whose src lookup -- read
 		// last iteration for the packets whose dst lookup decided nothing --
 		// R2 resolves first; one directions: W works on tile k-1)
-		const bool vW = BOTH ? (k >= 2 && tP - 2 * step < nt) : vR;
+		const bool vW = BOTH ? (k >= LAG + 1 && tP - (LAG + 1) * step < nt) : vR;
 		if constexpr (BOTH) {
 			PMARK("R2");
 			// lookup_verdict_ipv4 (xdpfilt_prog.h:121-134): the src key
@@ -344,25 +357,25 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			// matches.  A miss in a bucket marked overflowed may be a key
 			// that did not fit: the canonical table decides it (deferred).
 			// the halves to their packet's lane (see L): lane i < 32 holds
-			// half 0 of packet i in bk0 and half 1 of packet i in lane
-			// i + 32 of bk0; lanes i + 32 likewise in bk1 for packet 32 + i
+			// half 0 of packet i in rs.bk0 and half 1 of packet i in lane
+			// i + 32 of rs.bk0; lanes i + 32 likewise in rs.bk1 for packet 32 + i
 			bool found;
 			uint32_t ix;
-			const bool ovf = match(bk0, bk1, r_key, found, ix);
-			found &= r_sel;
-			const bool defer = r_sel & !found & ovf;
-			const uint32_t slot = r_b * XFG_QT_SLOTS + ix;
+			const bool ovf = match(rs.bk0, rs.bk1, rs.key, found, ix);
+			found &= rs.sel;
+			const bool defer = rs.sel & !found & ovf;
+			const uint32_t slot = rs.b * XFG_QT_SLOTS + ix;
 			const uint32_t x_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
-			const uint32_t x_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, r_tag));
+			const uint32_t x_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, rs.tag));
 			const uint32_t x_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
 			if constexpr (BOTH) {   // to R2 next iteration
-				q_need = r_sel & !found & !defer;
+				q_need = rs.sel & !found & !defer;
 				q_act = x_act;
 				q_tag = x_tag;
 				q_ps = x_ps;
 				q_len = r_len;
-				q_key2 = r_key2;
-				q_b2 = pick(q_need, r_b2, 0u);
+				q_key2 = rs.key2;
+				q_b2 = pick(q_need, rs.b2, 0u);
 			} else {
 				w_act = x_act;
 				w_tag = x_tag;
@@ -389,7 +402,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		PMARK("W");
 		// ---- W: verdicts, counters, stats, deferrals of tile k-1 (k-2)
 		if (vW) {
-			const uint32_t gi = (tP - (BOTH ? 2 : 1) * step) * 64 + lane;
+			const uint32_t gi = (tP - (LAG + (BOTH ? 1 : 0)) * step) * 64 + lane;
 			if (w_act <= A_PASS && !(dg & 8)) {
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
 			}
@@ -457,31 +470,31 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		if (!(dg & 2)) {
 			const auto ab = __builtin_amdgcn_permlane32_swap(lbk, lbk, false, false);
 			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
-			bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
-			bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
+			rs.bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
+			rs.bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
 		}
 		__builtin_amdgcn_sched_barrier(0);
 		PMARK("P");
 		// ---- P: parse tile k, hash its key, plan its fallback
 		if (vP && (dg & 64)) {   // (diagnostics: no parse)
 			const uint32_t gi = tP * 64 + lane;
-			r_b = pick(gi < n, hk >> rsh, 0u);
-			r_key = XFG_QT_USED | (hk & rmask);
-			r_sel = gi < n;
-			r_pk = pk3(pick(gi < n, MISS, A_NONE), XFG_PORT_TAB, len);
-			r_tag = CT_NONE;
+			rs.b = pick(gi < n, hk >> rsh, 0u);
+			rs.key = XFG_QT_USED | (hk & rmask);
+			rs.sel = gi < n;
+			rs.pk = pk3(pick(gi < n, MISS, A_NONE), XFG_PORT_TAB, len);
+			rs.tag = CT_NONE;
 		} else if (vP) {
 			const uint32_t gi = tP * 64 + lane;
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
 			const bool kok = valid & !r.defer & r.v4ok & klive;
 			const uint32_t h = hk;
-			r_b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
-			r_key = XFG_QT_USED | (h & rmask);
-			r_sel = kok;
+			rs.b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
+			rs.key = XFG_QT_USED | (h & rmask);
+			rs.sel = kok;
 			if constexpr (BOTH) {
-				r_b2 = pick(kok, hk2 >> rsh, 0u);
-				r_key2 = XFG_QT_USED | (hk2 & rmask);
+				rs.b2 = pick(kok, hk2 >> rsh, 0u);
+				rs.key2 = XFG_QT_USED | (hk2 & rmask);
 			}
 			uint32_t fa = pick(r.abort_at != NST, A_ABORTED, MISS), ft = CT_NONE, fs = XFG_PORT_TAB;
 			if constexpr (PORTS) {
@@ -509,14 +522,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 					fa = pick(ph, HIT, fa);
 				}
 			}
-			r_pk = pk3(pick(!valid, A_NONE, pick(r.defer, A_DEFER, fa)),
+			rs.pk = pk3(pick(!valid, A_NONE, pick(r.defer, A_DEFER, fa)),
 				   pick(valid & !r.defer, fs, XFG_PORT_TAB), len);
-			r_tag = pick(valid & !r.defer, ft, CT_NONE);
+			rs.tag = pick(valid & !r.defer, ft, CT_NONE);
 		} else {
-			r_sel = false;
-			r_b = 0;
-			r_pk = pk3(A_NONE, XFG_PORT_TAB, 0);
-			r_tag = CT_NONE;
+			rs.sel = false;
+			rs.b = 0;
+			rs.pk = pk3(A_NONE, XFG_PORT_TAB, 0);
+			rs.tag = CT_NONE;
 		}
 
 		PMARK("I");
@@ -538,14 +551,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	}
 	// (one more with both directions: the last tile's src lookup resolves
 	// an iteration after its dst lookup)
-	const uint32_t iters = first < nt ? (nt - 1 - first) / step + (BOTH ? 3 : 2) : 0u;
+	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 1 + LAG + (BOTH ? 1 : 0) : 0u;
 	uint32_t k = 0;
 	for (; k + 1 < iters; k += 2) {
-		iteration(k, preA, lenA);
-		iteration(k + 1, preB, lenB);
+		iteration(k, preA, lenA, stA);
+		iteration(k + 1, preB, lenB, LAG == 2 ? stB : stA);
 	}
 	if (k < iters)
-		iteration(k, preA, lenA);
+		iteration(k, preA, lenA, stA);
 
 	if (dg & 2048)
 		ndef = 0;
