@@ -44,6 +44,12 @@ int xfg_launch_qt_fold(unsigned long long *qt_hits, const uint32_t *trans,
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
 #define XFG_HOST_REG_MAX 16 /* registered host buffers per context */
+/* host-resident classify: staging slots in flight (each: a chunk's copies,
+ * kernel and verdicts on its own stream; the host prepares the next chunk
+ * while the others move) */
+#ifndef HOST_SLOTS
+#define HOST_SLOTS 4
+#endif
 
 struct dev_map {           /* device arrays of one hash map */
 	uint8_t *buckets;      /* (nbuckets + 1) * 64 B: keys, per-device flags, meta */
@@ -96,11 +102,11 @@ struct xfg_dev {
 	 * whole-frame fallback staging (FB_BYTES) */
 	pthread_mutex_t host_lock;
 	struct hpool *pool;
-	uint8_t *hs_hbuf[2], *hs_dbuf[2], *hs_dv[2];
-	uint32_t *hs_hl[2], *hs_dl[2];
-	uint32_t *hs_fb[2], *hs_fbc[2], *hs_hfbc[2];
-	hipStream_t hs_st[2];
-	hipEvent_t hs_done[2];
+	uint8_t *hs_hbuf[HOST_SLOTS], *hs_dbuf[HOST_SLOTS], *hs_dv[HOST_SLOTS];
+	uint32_t *hs_hl[HOST_SLOTS], *hs_dl[HOST_SLOTS];
+	uint32_t *hs_fb[HOST_SLOTS], *hs_fbc[HOST_SLOTS], *hs_hfbc[HOST_SLOTS];
+	hipStream_t hs_st[HOST_SLOTS];
+	hipEvent_t hs_done[HOST_SLOTS];
 	uint8_t *fb_h, *fb_d, *fb_dv;   /* fallback frames (pinned / device), verdicts */
 	uint64_t *fb_ho, *fb_do;        /* their offsets */
 	uint32_t *fb_hl, *fb_dl, *fb_idx;
@@ -355,7 +361,7 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->qt_hits);
 	free(d->port_flags_h);
 	hipFree(d->cstatus);
-	for (int k = 0; k < 2; k++) {
+	for (int k = 0; k < HOST_SLOTS; k++) {
 		if (d->hs_st[k])
 			hipStreamSynchronize(d->hs_st[k]);
 		hipHostFree(d->hs_hbuf[k]);
@@ -1784,9 +1790,10 @@ fail:
  * the ordinary device path afterwards -- the verdicts, counters and stats
  * are exactly those of a whole-frame run.  A fixed-stride batch whose
  * stride is at most HOST_WIN is staged slot for slot instead (one memcpy
- * per slice; nothing can fall back).  Two staging slots of HOST_CH packets
- * alternate (gather / H2D / kernel / D2H over two streams); their size is
- * fixed (HOST_CH x HOST_WIN bytes each), whatever the frames' lengths.
+ * per slice; nothing can fall back).  HOST_SLOTS staging slots of HOST_CH
+ * packets rotate (gather / H2D / kernel / D2H, each slot on its own
+ * stream); their size is fixed (HOST_CH x HOST_WIN bytes each), whatever
+ * the frames' lengths.
  * One lock per device: the devices' host paths run concurrently. */
 #define HOST_CH (1u << 18)     /* packets per staging slot */
 #define HOST_WIN 128u          /* header window (bytes) */
@@ -1864,7 +1871,7 @@ static int host_staging(struct xfg_dev *d)
 		return -ENOMEM;
 	if (d->hs_st[0])
 		return 0;
-	for (int k = 0; k < 2; k++) {
+	for (int k = 0; k < HOST_SLOTS; k++) {
 		HIPCHK(hipStreamCreateWithFlags(&d->hs_st[k], hipStreamNonBlocking));
 		HIPCHK(hipEventCreate(&d->hs_done[k]));
 		HIPCHK(hipHostMalloc((void **)&d->hs_hbuf[k], (size_t)HOST_CH * HOST_WIN,
@@ -1879,7 +1886,7 @@ static int host_staging(struct xfg_dev *d)
 	}
 	return 0;
 fail:
-	for (int k = 0; k < 2; k++) {   /* all or nothing: a later call starts over */
+	for (int k = 0; k < HOST_SLOTS; k++) {   /* all or nothing: a later call starts over */
 		if (d->hs_st[k])
 			hipStreamDestroy(d->hs_st[k]);
 		if (d->hs_done[k])
@@ -2082,13 +2089,15 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 	const int direct2d = !whole && !src->descs && !src->offsets && src->stride > HOST_WIN &&
 			     !(src->stride & 15) &&
 			     host_registered(ctx, src->data, n * (uint64_t)src->stride);
-	uint64_t pend[2] = { UINT64_MAX, UINT64_MAX };   /* each slot's last chunk */
+	uint64_t pend[HOST_SLOTS];   /* each slot's last chunk */
+	for (int k = 0; k < HOST_SLOTS; k++)
+		pend[k] = UINT64_MAX;
 
 	pthread_mutex_lock(&d->host_lock);
 	HIPCHK(hipSetDevice(d->ordinal));
 	if ((err = host_staging(d)))
 		goto fail;
-	for (uint64_t c = 0, k = 0; c < n; c += HOST_CH, k ^= 1) {
+	for (uint64_t c = 0, k = 0; c < n; c += HOST_CH, k = (k + 1) % HOST_SLOTS) {
 		const uint64_t m = n - c < HOST_CH ? n - c : HOST_CH;
 		HIPCHK(hipEventSynchronize(d->hs_done[k]));   /* slot k free again */
 		if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
@@ -2114,13 +2123,13 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 		HIPCHK(hipEventRecord(d->hs_done[k], d->hs_st[k]));
 		pend[k] = whole ? UINT64_MAX : c;
 	}
-	for (int k = 0; k < 2; k++) {
+	for (int k = 0; k < HOST_SLOTS; k++) {
 		HIPCHK(hipStreamSynchronize(d->hs_st[k]));
 		if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
 			goto fail;
 	}
 fail:
-	for (int k = 0; k < 2; k++)   /* (after an error: nothing may still use them) */
+	for (int k = 0; k < HOST_SLOTS; k++)   /* (after an error: nothing may still use them) */
 		if (d->hs_st[k])
 			hipStreamSynchronize(d->hs_st[k]);
 	pthread_mutex_unlock(&d->host_lock);
