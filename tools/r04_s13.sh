@@ -7,3 +7,8 @@ XFG_LIB=$PWD/tools/abl/lag2.so timeout -k 10 200 python -u tools/ab_parity.py $o
 done
 TAG=s13 VARIANTS="lag1 lag2" ROUNDS=3 bash tools/r04_ab.sh
 bash tools/r04_pmc.sh
+for r in 1 2; do for v in c4base c4nw8; do
+XFG_LIB=$PWD/tools/abl/$v.so timeout -k 10 300 python -u tools/bench_configs.py c4 > gpurun_out/c4_${v}_$r.log 2>&1; grep config gpurun_out/c4_${v}_$r.log | cut -c1-200 | sed "s/^/$v r$r /"
+done; done
+timeout -k 10 300 python -u tools/edit_latency.py > gpurun_out/edit_latency.log 2>&1; tail -1 gpurun_out/edit_latency.log
+XFG_LIB=diag XFG_QT_PATCH=off timeout -k 10 300 python -u tools/edit_latency.py > gpurun_out/edit_latency_rebuild.log 2>&1; tail -1 gpurun_out/edit_latency_rebuild.log

@@ -701,6 +701,13 @@ static int qt_edit(xfg_ctx *ctx, uint64_t slot, const void *key, uint8_t old, ui
 	struct xfg_qt *q = &ctx->qt;
 	if (ctx->qt_dirty || !ctx->qt_gen || !q->img)
 		return 0;   /* (rebuilt before its next use anyway) */
+#ifdef XFG_DIAG
+	const char *po = getenv("XFG_QT_PATCH");   /* "off": every edit rebuilds (round 3) */
+	if (po && !strcmp(po, "off")) {
+		ctx->qt_dirty = 1;
+		return 0;
+	}
+#endif
 	/* per image: does the key enter or leave it */
 	int chg[2] = { 0, 0 }, any = 0;
 	for (uint32_t im = 0; im < q->nimg; im++) {

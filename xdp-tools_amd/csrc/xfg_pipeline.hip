@@ -57,12 +57,15 @@ constexpr uint32_t A_DEFER = 6;
 #ifndef XFG_QT_NW
 #define XFG_QT_NW 8
 #endif
-#define QT_WAVES(W) ((W) <= 64 ? XFG_QT_NW : 4)
+#ifndef XFG_QT_NW128   /* waves per workgroup, 128-byte windows */
+#define XFG_QT_NW128 4
+#endif
+#define QT_WAVES(W) ((W) <= 64 ? XFG_QT_NW : XFG_QT_NW128)
 #define QT_THREADS(W) (64 * QT_WAVES(W))
 #ifndef XFG_QT_WGCU   /* workgroups per CU the register bound assumes */
 #define XFG_QT_WGCU 1
 #endif
-#define QT_MINW(W) ((W) <= 64 ? (XFG_QT_WGCU * XFG_QT_NW + 3) / 4 : 2)
+#define QT_MINW(W) ((W) <= 64 ? (XFG_QT_WGCU * XFG_QT_NW + 3) / 4 : 2)   // (128: 8 waves a CU)
 
 // Key descriptor: kind | mask << 2 | zero << 4 | byte offset << 5.
 __device__ __forceinline__ uint32_t kd_kind(uint32_t d) { return d & 3; }
