@@ -1,5 +1,5 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_a0_gpu_multirank.py tests/test_gpu_io.py > gpurun_out/pytest_s13.log 2>&1; rc=$?; echo pytest rc=$rc; grep -E "passed|failed" gpurun_out/pytest_s13.log | tail -2; [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" gpurun_out/pytest_s13.log | head -20; exit $rc; }
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/test_a0_gpu_multirank.py tests/test_gpu_io.py tests/test_gpu_configs.py tests/test_gpu_qt.py > gpurun_out/pytest_s13.log 2>&1; rc=$?; echo pytest rc=$rc; grep -E "passed|failed" gpurun_out/pytest_s13.log | tail -2; [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" gpurun_out/pytest_s13.log | head -20; exit $rc; }
 timeout -k 10 400 python -u bench.py --steps 20 --no-cpu > gpurun_out/bench_s13.log 2>&1 || exit 3; python3 -c "
 import json;d=json.loads(open('gpurun_out/bench_s13.log').read().strip().split(chr(10))[-1]);print('bench',d['ms_per_step'],d['roofline']['frac'],d['host_path'])"
 for o in "" "--hot 8" "--src-dst"; do
@@ -12,3 +12,4 @@ XFG_LIB=$PWD/tools/abl/$v.so timeout -k 10 300 python -u tools/bench_configs.py 
 done; done
 timeout -k 10 300 python -u tools/edit_latency.py > gpurun_out/edit_latency.log 2>&1; tail -1 gpurun_out/edit_latency.log
 XFG_LIB=diag XFG_QT_PATCH=off timeout -k 10 300 python -u tools/edit_latency.py > gpurun_out/edit_latency_rebuild.log 2>&1; tail -1 gpurun_out/edit_latency_rebuild.log
+timeout -k 10 400 python -u tools/bench_configs.py c5 c3sd c3 > gpurun_out/cfg_s13.log 2>&1; grep config gpurun_out/cfg_s13.log | cut -c1-400

@@ -1564,7 +1564,11 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	/* (with the quotient index the log holds QT slots only: its span) */
 	uint64_t total = a.qt ? (uint64_t)a.qt_n : (uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES;
 	uint64_t hist = ((total + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
-	if (!log_off && hist <= XFG_LOG_HIST_MAX && grid <= XFG_LOG_SLICES_MAX) {
+	/* (a range past one histogram: the count kernel takes it in passes; past
+	 * 65536 local indices the slices hold u32) */
+	const int pwide = hist > 65536;
+	if (!log_off && hist <= (uint64_t)XFG_LOG_HIST_MAX * XFG_LOG_PASSES_MAX &&
+	    grid <= XFG_LOG_SLICES_MAX) {
 		/* slice (partition, workgroup): twice a uniform share of the
 		 * most the workgroup's waves can log (a fuller one spills) */
 		uint64_t wg_max = (per_wg / 64) * (uint64_t)a.defer_cap;
@@ -1574,7 +1578,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		if ((!a.qt && (err = scratch(d, (void **)&d->tlog, &d->tlog_bytes,
 					     grid * (per_wg / 64) * (uint64_t)a.defer_cap * 4))) ||
 		    (err = scratch(d, (void **)&d->pbuf, &d->pbuf_bytes,
-				   ((uint64_t)XFG_LOG_PARTS * grid * pcap + 512) * 2)) ||   /* (+ the count kernel's overread) */
+				   ((uint64_t)XFG_LOG_PARTS * grid * pcap + 1024) * (pwide ? 4 : 2))) ||   /* (+ the count kernel's overread) */
 		    (err = scratch(d, (void **)&d->pfill, &d->pfill_bytes,
 				   (uint64_t)XFG_LOG_PARTS * grid * 4)))
 			goto out;
@@ -1583,7 +1587,9 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.pfill = d->pfill;
 		a.pcap = (uint32_t)pcap;
 		a.pslices = (uint32_t)grid;
-		a.log_hist = (uint32_t)hist;
+		a.log_hist = (uint32_t)(hist < XFG_LOG_HIST_MAX ? hist : XFG_LOG_HIST_MAX);
+		a.log_span = (uint32_t)hist;
+		a.pwide = (uint32_t)pwide;
 	}
 	if (a.qt && !a.pbuf) {   /* (decided above: cannot happen) */
 		err = -EIO;

@@ -1036,7 +1036,10 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 			const uint32_t pos = s_cur[p] + (t - s_off[p]);
 			if (a.diag & 256)   // diagnostics build only: no write-out
 				continue;
-			if (pos < a.pcap)   // (the partition is implied: the local index)
+			if (pos < a.pcap && a.pwide)   // (the partition is implied: the local index)
+				*reinterpret_cast<__attribute__((address_space(1))) uint32_t *>(
+					(uintptr_t)(reinterpret_cast<uint32_t *>(a.pbuf) + p * pstep + slice0 + pos)) = log_local(x);
+			else if (pos < a.pcap)
 				*reinterpret_cast<__attribute__((address_space(1))) uint16_t *>(
 					(uintptr_t)(a.pbuf + p * pstep + slice0 + pos)) = (uint16_t)log_local(x);
 			else
@@ -1275,7 +1278,9 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 {
 	extern __shared__ uint32_t hist[];
 	__shared__ uint32_t s_fill[XFG_LOG_SLICES_MAX];
-	const uint32_t tid = threadIdx.x, p = blockIdx.x, lane = tid & 63, w = tid >> 6;
+	// (partition p, pass j: local indices [j * hist_n, (j + 1) * hist_n))
+	const uint32_t tid = threadIdx.x, p = blockIdx.x % XFG_LOG_PARTS, lane = tid & 63, w = tid >> 6;
+	const uint32_t j0 = (blockIdx.x / XFG_LOG_PARTS) * hist_n;
 	constexpr uint32_t NWV = LC_THREADS / 64, U = 8, J = XFG_LOG_HIST_MAX / LC_THREADS;
 	const uint32_t S = a.pslices, cap = a.pcap;
 	// the identity span: hash-map + port counters, or the QT slots
@@ -1287,9 +1292,10 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	auto ctr = [&](uint32_t g) { return a.qt_hits ? a.qt_hits + g : global_counter(a, g); };
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++) {
-		const uint32_t k = tid + j * LC_THREADS;
-		const uint32_t g = ((k >> 4) << 12) | (p << 4) | (k & 15);
-		gid[j] = k < hist_n && g < total ? (a.qt_hits ? g : a.qt ? a.qt_trans[g] : g) : CT_NONE;
+		const uint32_t k = tid + j * LC_THREADS, l = j0 + k;
+		const uint32_t g = ((l >> 4) << 12) | (p << 4) | (l & 15);
+		gid[j] = k < hist_n && l < a.log_span && g < total ? (a.qt_hits ? g : a.qt ? a.qt_trans[g] : g)
+								   : CT_NONE;
 	}
 	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * S + tid] : 0u;
 	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
@@ -1305,38 +1311,52 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	if (tid < S)
 		s_fill[tid] = min(fl, cap);
 	__syncthreads();
+	if (a.pwide) {   // (u32 local indices, a range beyond one pass)
+		const uint32_t *wb = reinterpret_cast<const uint32_t *>(a.pbuf) + (uint64_t)p * S * cap;
+		for (uint32_t sl = w; sl < S; sl += NWV) {
+			const uint32_t np = s_fill[sl];
+			for (uint32_t i = lane; i < np; i += 64) {
+				const uint32_t l = __builtin_nontemporal_load(wb + (uint64_t)sl * cap + i) - j0;
+				if (l < hist_n)
+					atomicAdd(&hist[l], 1u);
+			}
+		}
+	}
 	const uint16_t *base = a.pbuf + (uint64_t)p * S * cap;
-	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-	auto add4 = [&](u32x2 v, uint32_t i0, uint32_t np) {
+	// (a wave load covers 512 entries of a slice -- 16 bytes a lane: about a
+	// uniform slice at the bench's batch; pcap is a multiple of 8, so every
+	// slice starts 16-byte aligned; the buffer has 512 entries of slack)
+	auto add8 = [&](u32x4 v, uint32_t i0, uint32_t np) {
 #pragma unroll
-		for (uint32_t c = 0; c < 2; c++) {
-			if (i0 + 2 * c < np)
-				atomicAdd(&hist[v[c] & 0xffff], 1u);
-			if (i0 + 2 * c + 1 < np)
-				atomicAdd(&hist[v[c] >> 16], 1u);
+		for (uint32_t c = 0; c < 4; c++) {
+			const uint32_t l0 = (v[c] & 0xffff) - j0, l1 = (v[c] >> 16) - j0;
+			if (i0 + 2 * c < np && l0 < hist_n)
+				atomicAdd(&hist[l0], 1u);
+			if (i0 + 2 * c + 1 < np && l1 < hist_n)
+				atomicAdd(&hist[l1], 1u);
 		}
 	};
-	for (uint32_t s0 = w; s0 < S; s0 += NWV * U) {
-		u32x2 v[U];
+	for (uint32_t s0 = a.pwide ? S : w; s0 < S; s0 += NWV * U) {
+		u32x4 v[U];
 #pragma unroll
 		for (uint32_t u = 0; u < U; u++) {
 			const uint32_t sl = s0 + u * NWV;
-			const u32x2 *e = (const u32x2 *)(base + (uint64_t)sl * cap);
-			v[u] = sl < S ? __builtin_nontemporal_load(e + lane) : u32x2{ 0, 0 };
+			const u32x4 *e = (const u32x4 *)(base + (uint64_t)sl * cap);
+			v[u] = sl < S && s_fill[sl] ? __builtin_nontemporal_load(e + lane) : u32x4{ 0, 0, 0, 0 };
 		}
 #pragma unroll
 		for (uint32_t u = 0; u < U; u++) {
 			const uint32_t sl = s0 + u * NWV;
-			add4(v[u], lane * 4, sl < S ? s_fill[sl] : 0u);
+			add8(v[u], lane * 8, sl < S ? s_fill[sl] : 0u);
 		}
 		// (a fuller slice: the rest)
 #pragma unroll
 		for (uint32_t u = 0; u < U; u++) {
 			const uint32_t sl = s0 + u * NWV;
 			const uint32_t np = sl < S ? s_fill[sl] : 0u;
-			const u32x2 *e = (const u32x2 *)(base + (uint64_t)sl * cap);
-			for (uint32_t i = 256 + lane * 4; i < np; i += 256)
-				add4(__builtin_nontemporal_load(e + i / 4), i, np);
+			const u32x4 *e = (const u32x4 *)(base + (uint64_t)sl * cap);
+			for (uint32_t i = 512 + lane * 8; i < np; i += 512)
+				add8(__builtin_nontemporal_load(e + i / 8), i, np);
 		}
 	}
 	__syncthreads();
@@ -1448,7 +1468,8 @@ extern "C" int xfg_launch_log_count(const struct xfg_kargs *a, void *stream)
 {
 	if (!a->pbuf)
 		return 0;
-	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS), dim3(LC_THREADS),
+	const uint32_t passes = (a->log_span + a->log_hist - 1) / a->log_hist;
+	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS * passes), dim3(LC_THREADS),
 			   (size_t)a->log_hist * 4, static_cast<hipStream_t>(stream), *a, a->log_hist);
 	return hipGetLastError() == hipSuccess ? 0 : -(int)hipGetLastError() - 1000;
 }

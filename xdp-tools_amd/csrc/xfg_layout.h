@@ -95,6 +95,7 @@
 #define XFG_DCNT_MAX      4096u   /* direct LDS counters (16 KiB) */
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
 #define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
+#define XFG_LOG_PASSES_MAX 32u    /* histogram passes per partition (span 512K) */
 #define XFG_LOG_SLICES_MAX 1024u  /* slices per partition: classify workgroups */
 #define XFG_LOG_MIN_KEYS  256u    /* fewer hash-map keys: LDS counter cache, no log */
 
@@ -166,6 +167,11 @@ struct xfg_kargs {
 	uint32_t pcap;
 	uint32_t pslices;
 	uint32_t log_hist;
+	/* a partition's local-index range (log_span) beyond one histogram: the
+	 * count kernel takes it in passes of log_hist (one workgroup per
+	 * partition and pass); past 65536 the slices hold u32 indices (pwide) */
+	uint32_t log_span;
+	uint32_t pwide;
 	/* Pipelined kernel: deferred packets, defer_cap entries per wave */
 	uint32_t *defer;
 	uint32_t defer_cap;
