@@ -12,8 +12,8 @@ per-action stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
       64 B frames, 2^22 packets (the IPv4-key pipelined kernel, hit log)
   C4  xdpfilt_dny_all, IMIX 64/570/1514 at a 1536 B stride, 1M IPv4 rules
   C5  xdpfilt_dny_all, 15M IPv4 + 1M IPv6 dst rules + 1024 dst-port rules,
-      1514 B frames at a 1536 B stride, 2^18 packets, device-resident and
-      through xfg_classify_host
+      1514 B frames at a 1536 B stride, 2^18 packets, device-resident (the
+      quotient-index kernel) and through xfg_classify_host
 """
 import numpy as np
 import pytest
@@ -49,12 +49,14 @@ def config_rules(kind, n4, n6, nports, port_rules=True):
     return rules, v4, v6, ports
 
 
-def check(G, variant, rules, data, lens, stride, host=False, **caps):
+def check(G, variant, rules, data, lens, stride, host=False, path=None, **caps):
     ov, orules, ost = X.run_oracle(X.VARIANT_FEATURES[variant], data, lens, rules,
                                    stride=stride, nthreads=8)
     f = make_filter(G, variant, **caps)
     f.load_rules(rules)
     v = f.run(data, lens, stride=stride)
+    if path is not None:
+        assert f.last_path() == path
     assert_same(v, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
     f.close()
     if host:
@@ -108,5 +110,7 @@ def test_c4_imix_1536_stride(G):
 def test_c5_16m_rules_1514b_device_and_host(G):
     rules, v4, v6, ports = config_rules(5, 15_000_000, 1_000_000, 1024)
     data, lens = X.gen_workload(5, 5, 1 << 18, 1536, v4=v4, v6=v6, ports=ports)
-    check(G, "xdpfilt_dny_all", rules, data, lens, 1536, host=True,
+    # (the quotient index of 2^21 buckets: u32 hit-log entries, eight count
+    # passes; the IPv6 frames through the deferred path)
+    check(G, "xdpfilt_dny_all", rules, data, lens, 1536, host=True, path=5,
           ipv4_capacity=15_000_000, ipv6_capacity=1_000_000)

@@ -416,3 +416,57 @@ def test_qt_hits_concentrated_in_few_log_partitions(G, stride):
     rules.v4_vals = np.full(len(keys), 2, np.uint64)
     data, lens = X.gen_workload(82, 3, 1 << 20, stride, v4=keys, dst_permille=700)
     run_both(G, "xdpfilt_dny_all", rules, data, lens, stride)
+
+
+@pytest.mark.parametrize("variant", ["xdpfilt_dny_all", "xdpfilt_alw_all", "xdpfilt_dny_ip"])
+@pytest.mark.parametrize("stride", [64, 128, 1536])
+def test_qt_with_ipv6_rules_defers_ipv6_frames(G, variant, stride):
+    """IPv6 rules beside the IPv4 map (C5's shape, no Ethernet rule): the
+    index kernel still takes the batch, every IPv6 frame goes to its
+    deferred path -- the whole walk over the canonical tables (dst then src,
+    xdpfilt_prog.h:152-165) -- and the IPv4 lookups stay on the index."""
+    rng = np.random.default_rng(101)
+    rules, v4, ports = one_direction_rules(102, 20000, 2)
+    v6 = X.rand_keys(103, 4000, 16)
+    rules.v6_keys = v6
+    f6 = np.where(rng.random(len(v6)) < 0.5, 2, 1).astype(np.uint64)   # dst or src rules
+    f6[rng.random(len(v6)) < 0.1] |= 4
+    rules.v6_vals = f6 | (rng.integers(0, 50, len(v6)).astype(np.uint64) << 6)
+    kind = 5 if stride == 1536 else 3
+    d1, l1 = X.gen_workload(104, kind, 1 << 15, stride, v4=v4, v6=v6, ports=ports)
+    d2, l2 = fuzz_at(105, 1 << 14, stride, rules, ports)
+    data = np.concatenate([d1, d2])
+    lens = np.concatenate([l1, l2])
+    ov = run_both(G, variant, rules, data, lens, stride, ipv6_capacity=1 << 13)
+    assert len(np.unique(ov)) == 3
+
+
+def test_qt_not_taken_with_ethernet_rules_live(G):
+    """An Ethernet rule is tested on every frame before its IP keys
+    (xdpfilt_prog.h:187-196): the index kernel, which carries IPv4 keys only,
+    does not take such a batch (the general pipelined kernel does)."""
+    rules, v4, ports = one_direction_rules(111, 20000, 2)
+    rules.eth_keys = np.array([[2, 0, 0, 0, 0, 1]], np.uint8)
+    rules.eth_vals = np.array([2], np.uint64)
+    data, lens = X.gen_workload(112, 3, 1 << 15, 64, v4=v4, ports=ports)
+    run_both(G, "xdpfilt_dny_all", rules, data, lens, 64, path=1, eth_capacity=16)
+
+
+@pytest.mark.timeout(300)
+def test_qt_index_past_one_count_pass(G):
+    """3M IPv4 rules: an index of 2^19 buckets, whose hit log the count
+    kernel takes in two passes of its LDS histogram (u16 local indices)."""
+    n4 = 3_000_000
+    v4 = X.rand_keys(121, int(n4 * 1.02) + 16, 4)[:n4]
+    rules = X.RuleSet()
+    rules.v4_keys = v4
+    rules.v4_vals = np.full(len(v4), 2, np.uint64)
+    data, lens = X.gen_workload(122, 3, 1 << 20, 64, v4=v4, dst_permille=600)
+    ov, orules, ost = X.run_oracle(X.VARIANT_FEATURES["xdpfilt_dny_all"], data, lens, rules,
+                                   stride=64, nthreads=8)
+    f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=n4)
+    f.load_rules(rules)
+    v = f.run(data, lens, stride=64)
+    assert f.last_path() == 5
+    assert_same(v, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
+    f.close()

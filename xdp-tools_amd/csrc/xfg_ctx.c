@@ -1236,11 +1236,19 @@ int xfg_map_update_batch_percpu(xfg_ctx *ctx, int map, const void *keys, const u
 static int port_tab_refresh_locked(struct xfg_dev *d);
 
 
-/* Whether the count kernel's LDS histogram covers a QT of 2^bits buckets. */
-static int qt_hist_fits(uint32_t bits)
+/* A partition's local-index range of a hit log over @span QT slots. */
+static uint64_t qt_log_hist(uint64_t span)
 {
-	const uint64_t span = (1ull << bits) * XFG_QT_SLOTS;
-	return ((span + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16 <= XFG_LOG_HIST_MAX;
+	return ((span + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
+}
+
+/* Whether the count kernel covers the hit log of a QT of @span slots: in
+ * passes of its LDS histogram (u32 local indices past 65536), or with both
+ * lookup directions in one pass (that kernel logs u16 indices only). */
+static int qt_log_fits(uint64_t span, int both)
+{
+	const uint64_t h = qt_log_hist(span);
+	return both ? h <= XFG_LOG_HIST_MAX : h <= (uint64_t)XFG_LOG_HIST_MAX * XFG_LOG_PASSES_MAX;
 }
 
 static int port_tab_refresh(struct xfg_dev *d)
@@ -1366,6 +1374,11 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	 * stride; everything else stages 128 bytes (every synthetic class and all
 	 * common headers parse within 78 bytes; a longer parse reads HBM). */
 	a->window = (!b->offsets && b->stride && b->stride <= 64) ? 64 : 128;
+#ifdef XFG_DIAG
+	const char *wn = getenv("XFG_WINDOW");   /* "64": 64-byte windows at any stride */
+	if (wn && !strcmp(wn, "64"))
+		a->window = 64;
+#endif
 	/* The pipelined kernel takes every fixed-stride batch whose windows can
 	 * be loaded without a length (stride >= window, 16-byte aligned; packet
 	 * indices fit its 32-bit deferred lists); the general kernel the rest. */
@@ -1382,6 +1395,10 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	int eth_live = (ctx->prog_features & XFG_FEAT_ETHERNET) && a->te.count && (a->te.fmask & 3);
 	int v6_live = (ctx->prog_features & XFG_FEAT_IPV6) && a->t6.count && (a->t6.fmask & 3);
 	a->km = (ctx->prog_features & XFG_FEAT_IPV4) && !eth_live && !v6_live;
+	/* (IPv6 keys live, Ethernet keys not: the quotient-index kernel may still
+	 * take the batch, sending every IPv6 frame to its deferred path) */
+	const int km6 = (ctx->prog_features & XFG_FEAT_IPV4) && !eth_live && v6_live;
+	a->v6d = 0;
 	/* per-lane u32 byte sums in the pipelined kernel: bound them */
 	if (a->pipe && (uint64_t)a->stride * (((b->count + 63) / 64 + 1023) / 1024 + 1) >= (1ull << 32))
 		a->pipe = 0;
@@ -1405,11 +1422,12 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	 * one live IPv4 lookup direction, the same flags on every device, and a
 	 * map large enough that the prefilter + bucket-line chain leaves L2;
 	 * its hit log must fit the count kernel's histogram */
-	if (a->pipe && a->km && !a->split) {
+	if (a->pipe && (a->km || km6) && !a->split) {
 		/* (both directions live: up to two images, twice the QT slots) */
 		const int dl = a->t4.count && (a->t4.fmask & 2), sl = a->t4.count && (a->t4.fmask & 1);
 		const int ok = (dl | sl) && !ctx->flag_cnt[0][7] &&
-			       qt_hist_fits(xfg_qt_bits_for(a->t4.count) + (dl & sl));
+			       qt_log_fits(((uint64_t)XFG_QT_SLOTS << xfg_qt_bits_for(a->t4.count)) << (dl & sl),
+					   dl & sl);
 		int use = ok && a->t4.count >= ctx->qt_min_keys;
 #ifdef XFG_DIAG
 		const char *qo = getenv("XFG_QT");   /* "off" / "on" (any size) */
@@ -1423,6 +1441,10 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 			if (err2)
 				return err2;
 			a->qt = d->qt_img;   /* (parameters: launch_batch, under d->lock) */
+			if (!a->km) {
+				a->km = 1;
+				a->v6d = 1;
+			}
 		}
 	}
 	return 0;
@@ -1491,10 +1513,12 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		uint64_t g5 = (uint64_t)d->ncu * (pc > 0 ? pc : 1), need5 = (a.n + pw - 1) / pw;
 		if (g5 > need5)
 			g5 = need5 ? need5 : 1;
-		const uint64_t span = (uint64_t)d->qt_n;
-		const uint64_t hist5 = ((span + 16 * XFG_LOG_PARTS - 1) / (16 * XFG_LOG_PARTS)) * 16;
-		if (log_off || g5 > XFG_LOG_SLICES_MAX || hist5 > XFG_LOG_HIST_MAX)
+		if (log_off || g5 > XFG_LOG_SLICES_MAX || !qt_log_fits(d->qt_n, d->qt_live == 3))
 			a.qt = NULL;
+	}
+	if (!a.qt && a.v6d) {   /* (the IPv6 keys need the general kernel then) */
+		a.km = 0;
+		a.v6d = 0;
 	}
 	const int kind = a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
 	if (a.qt) {   /* the index in stream order at this launch */

@@ -1368,27 +1368,30 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	}
 }
 
-template <uint32_t FEAT, bool L16, bool BOTH>
+template <uint32_t FEAT, bool L16, bool BOTH, bool WIDE>
 void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
 	if (a.window <= 64 && a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
 	else if (a.window <= 64)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
 	else if (a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 	else
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 }
 
-// (qt_live 3: both IPv4 lookups through the index)
+// (qt_live 3: both IPv4 lookups through the index; pwide: an index past
+// 2^20 buckets, one lookup direction -- the host takes no other)
 template <uint32_t FEAT, bool L16>
 void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
 	if (a.qt_live == 3)
-		launch_pipeq2<FEAT, L16, true>(a, grid, dl, s);
+		launch_pipeq2<FEAT, L16, true, false>(a, grid, dl, s);
+	else if (a.pwide)
+		launch_pipeq2<FEAT, L16, false, true>(a, grid, dl, s);
 	else
-		launch_pipeq2<FEAT, L16, false>(a, grid, dl, s);
+		launch_pipeq2<FEAT, L16, false, false>(a, grid, dl, s);
 }
 
 template <uint32_t FEAT>
@@ -1471,7 +1474,8 @@ extern "C" int xfg_launch_log_count(const struct xfg_kargs *a, void *stream)
 	const uint32_t passes = (a->log_span + a->log_hist - 1) / a->log_hist;
 	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS * passes), dim3(LC_THREADS),
 			   (size_t)a->log_hist * 4, static_cast<hipStream_t>(stream), *a, a->log_hist);
-	return hipGetLastError() == hipSuccess ? 0 : -(int)hipGetLastError() - 1000;
+	const hipError_t e = hipGetLastError();
+	return e == hipSuccess ? 0 : -(int)e - 1000;
 }
 
 extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a,
@@ -1532,8 +1536,8 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 		} else if (kind == 5) {
 			done = true;
 			e = window <= 64
-				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true, false>, QT_THREADS(64), dyn)
-				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true, false>, QT_THREADS(128), dyn);
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true, false, false>, QT_THREADS(64), dyn)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true, false, true>, QT_THREADS(128), dyn);
 		}
 	}
 	if (done)

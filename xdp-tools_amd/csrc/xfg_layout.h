@@ -151,6 +151,9 @@ struct xfg_kargs {
 	uint32_t dense;               /* pipelined kernel: stride == window */
 	uint32_t pipe;                /* the pipelined kernel (fixed stride >= window) */
 	uint32_t km;                  /* pipelined key mode: 1 = only IPv4 keys are live */
+	/* quotient-index kernel with IPv6 keys live (no Ethernet key): every IPv6
+	 * frame goes to the deferred path, the IPv4 lookups through the index */
+	uint32_t v6d;
 	/* Direct LDS counters: identities below dcnt (all hash maps, gbase[3],
 	 * or the IPv4 map, gbase[1]) are summed per workgroup in LDS; 0 = off */
 	uint32_t dcnt;

@@ -716,7 +716,7 @@ namespace {
 
 struct Parse4 {
 	uint32_t abort_at, l4proto, psrc, pdst, k4a, k4b;
-	bool v4ok, defer;
+	bool v4ok, defer, is6;
 };
 
 // Branch-free helpers: every operand evaluated, combined with bitwise
@@ -787,6 +787,7 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	r.k4a = __builtin_amdgcn_alignbyte(d8, d7, 2);   // daddr 30..33
 	r.k4b = __builtin_amdgcn_alignbyte(d7, d6, 2);   // saddr 26..29
 	r.v4ok = !runt & is4 & !s4 & !ihlx;
+	r.is6 = !runt & is6;
 	return r;
 }
 

@@ -43,6 +43,9 @@
 #ifndef XFG_QT_LAG       /* iterations between a tile's bucket loads and their match */
 #define XFG_QT_LAG 1
 #endif
+#ifndef XFG_QT_DEPTH     /* tiles of windows in flight per wave (3: with XFG_QT_LAG 2 only) */
+#define XFG_QT_DEPTH 2
+#endif
 #ifndef XFG_QT_WC_R      /* ring entries per partition, 64-byte windows */
 #define XFG_QT_WC_R 128
 #endif
@@ -55,7 +58,7 @@
 
 namespace {
 
-template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH>
+template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE>
 __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
 	static_assert((FEAT & F_IPV4) != 0, "IPv4-key mode needs the IPv4 feature");
@@ -67,6 +70,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t LAG = XFG_QT_LAG;
 	static_assert(LAG == 1 || LAG == 2, "bucket lag: one or two iterations");
+	// (both directions: the src buckets loaded in R are matched the next
+	// iteration, so a third tile of windows could not stay in flight)
+	constexpr uint32_t D = BOTH ? 2u : XFG_QT_DEPTH;
+	static_assert(D == 2 || (D == 3 && LAG == 2), "window depth: 2, or 3 with a bucket lag of 2");
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	constexpr uint32_t QTAG = CT_QTAG;   // tag bit: a QT slot (hit log), not a counter identity
 	// Write-combined hit log.  A QT hit of partition p = log_part(slot)
@@ -81,11 +88,15 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// that would overrun the slice.  No per-wave log, no workgroup-end sort.
 	constexpr uint32_t PPW = XFG_LOG_PARTS / NW;   // partitions a wave owns: lane * NW + wave
 	static_assert(PPW * NW == XFG_LOG_PARTS && PPW <= 64, "partition ownership");
-	constexpr uint32_t WR = W <= 64 ? XFG_QT_WC_R : XFG_QT_WC_R128;
-	constexpr uint32_t WF = W <= 64 ? XFG_QT_WC_F : WR / 2;   // flush chunk
+	// (WIDE: an index past 2^20 buckets -- local indices past 16 bits -- logs
+	// u32 entries, a ring of the same bytes: half the entries; with 64-byte
+	// windows a flush chunk is still a line)
+	typedef typename std::conditional<WIDE, uint32_t, uint16_t>::type ring_t;
+	constexpr uint32_t WR = (W <= 64 ? XFG_QT_WC_R : XFG_QT_WC_R128) / (WIDE ? 2 : 1);
+	constexpr uint32_t WF = W <= 64 ? XFG_QT_WC_F / (WIDE ? 2 : 1) : WR / 2;   // flush chunk
 	static_assert((WR & (WR - 1)) == 0 && WF <= 64, "ring: a power of two");
 	__shared__ uint32_t win[NW * 64 * ROWDW];
-	__shared__ uint16_t s_ring[XFG_LOG_PARTS * WR];
+	__shared__ ring_t s_ring[XFG_LOG_PARTS * WR];
 	__shared__ uint32_t s_res[XFG_LOG_PARTS];
 	__shared__ __attribute__((aligned(8))) uint32_t s_hd[2 * XFG_LOG_PARTS];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
@@ -116,6 +127,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const uint64_t qb2 = BOTH ? rfl64((uint64_t)(uintptr_t)a.qt2) : 0;
 	const uint32_t qbase2 = BOTH ? rfl(a.qt_base) : 0u;
 	const bool klive = a.t4.count != 0;
+	// (IPv6 keys live, no Ethernet key: every IPv6 frame takes the deferred
+	// path -- the whole reference walk over the canonical tables)
+	const bool v6d = (FEAT & F_IPV6) != 0 && a.v6d != 0;
 	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
 	cn.init(a, tid, NT);
 	if (tid < 6)
@@ -162,7 +176,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				const uint32_t r = atomicAdd(&s_res[p], 1u);
 				if (r < WR) {
 					const uint32_t t = atomicAdd(&s_hd[2 * p], 1u);
-					s_ring[p * WR + (t & (WR - 1))] = (uint16_t)log_local(qs);
+					s_ring[p * WR + (t & (WR - 1))] = (ring_t)log_local(qs);
 					atomicAdd(&s_hd[2 * p + 1], 1u);
 				} else {   // the ring is full: the LDS counter cache
 					atomicSub(&s_res[p], 1u);
@@ -186,8 +200,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const uint32_t e = s_ring[p * WR + ((fl + o) & (WR - 1))];
 			const uint32_t pos = fl + o;
 			if (pos < a.pcap)
-				*reinterpret_cast<__attribute__((address_space(1))) uint16_t *>(
-					(uintptr_t)(a.pbuf + p * wc_pstep + wc_slice0 + pos)) = (uint16_t)e;
+				*reinterpret_cast<__attribute__((address_space(1))) ring_t *>(
+					(uintptr_t)(reinterpret_cast<ring_t *>(a.pbuf) + p * wc_pstep + wc_slice0 + pos)) = (ring_t)e;
 			else {
 				const uint32_t g = ((e >> 4) << 12) | (p << 4) | (e & 15);
 				if (!cache_hit(cn.ctag, cn.ccnt, QTAG | g, 1))
@@ -311,14 +325,17 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 		return (w[7] >> 16) == XFG_QT_OVF_MARK;
 	};
-	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen, RSt &rs) {
+	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen, RSt &rs) __attribute__((always_inline)) {
 		const uint32_t tP = first + k * step;
 		const bool vP = tP < nt;
 		const bool vR = k >= LAG && tP - LAG * step < nt;
 		// everything but the newest iteration's loads (LAG 1: tile k+1's
-		// windows; LAG 2: also the last iteration's bucket loads)
-		constexpr uint32_t VW = CPP + 1 + (LAG - 1) * 2;
+		// windows; LAG 2: also the last iteration's bucket loads; depth 3:
+		// also the windows issued the iteration before)
+		constexpr uint32_t VW = CPP + 1 + (LAG - 1) * 2 + (D - 2) * (CPP + 1);
 		__builtin_amdgcn_s_waitcnt(0x0F70 | (VW & 15) | ((VW >> 4) << 14));
+		if constexpr (D == 3)   // (nothing that uses a load above the wait)
+			__builtin_amdgcn_sched_barrier(0);
 		// (the length is used from here on: without this the compiler
 		// rotates its zero-extension to the previous iteration's end, where
 		// it waits for the load -- and every older one -- early)
@@ -487,7 +504,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const uint32_t gi = tP * 64 + lane;
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
-			const bool kok = valid & !r.defer & r.v4ok & klive;
+			const bool rdef = r.defer | (v6d & r.is6);
+			const bool kok = valid & !rdef & r.v4ok & klive;
 			const uint32_t h = hk;
 			rs.b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
 			rs.key = XFG_QT_USED | (h & rmask);
@@ -522,9 +540,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 					fa = pick(ph, HIT, fa);
 				}
 			}
-			rs.pk = pk3(pick(!valid, A_NONE, pick(r.defer, A_DEFER, fa)),
-				   pick(valid & !r.defer, fs, XFG_PORT_TAB), len);
-			rs.tag = pick(valid & !r.defer, ft, CT_NONE);
+			rs.pk = pk3(pick(!valid, A_NONE, pick(rdef, A_DEFER, fa)),
+				   pick(valid & !rdef, fs, XFG_PORT_TAB), len);
+			rs.tag = pick(valid & !rdef, ft, CT_NONE);
 		} else {
 			rs.sel = false;
 			rs.b = 0;
@@ -533,32 +551,78 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 
 		PMARK("I");
-		// ---- tile k+2's windows, last: in flight for two iterations
+		// ---- tile k+D's windows, last: in flight for D iterations
 		// (issued before the parse instead, the compiler's register
 		// reuse puts waits into R: not kept)
 		__builtin_amdgcn_sched_barrier(0);
-		issue(tP + 2 * step, cur, curlen);
+		issue(tP + D * step, cur, curlen);
 		__builtin_amdgcn_sched_barrier(0);
 	};
 
-	u32x4 preA[CPP], preB[CPP];
-	len_t lenA = 0, lenB = 0;
+	u32x4 preA[CPP], preB[CPP], preC[D == 3 ? CPP : 1];
+	len_t lenA = 0, lenB = 0, lenC = 0;
 	if (nt) {
 		issue(first, preA, lenA);
 		__builtin_amdgcn_sched_barrier(0);
 		issue(first + step, preB, lenB);
 		__builtin_amdgcn_sched_barrier(0);
+		if constexpr (D == 3) {
+			issue(first + 2 * step, preC, lenC);
+			__builtin_amdgcn_sched_barrier(0);
+		}
 	}
 	// (one more with both directions: the last tile's src lookup resolves
 	// an iteration after its dst lookup)
 	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 1 + LAG + (BOTH ? 1 : 0) : 0u;
-	uint32_t k = 0;
-	for (; k + 1 < iters; k += 2) {
-		iteration(k, preA, lenA, stA);
-		iteration(k + 1, preB, lenB, LAG == 2 ? stB : stA);
+	// iteration k uses window buffer k % D and state set k % LAG: the loop
+	// body is U = lcm(D, LAG) iterations
+	constexpr uint32_t U = D == 3 ? 3 * LAG : 2;
+	auto one = [&](uint32_t k, auto uc) __attribute__((always_inline)) {
+		constexpr uint32_t u = decltype(uc)::value;
+		RSt &rs = (LAG == 2 && (u & 1)) ? stB : stA;
+		if constexpr (u % D == 0)
+			iteration(k, preA, lenA, rs);
+		else if constexpr (u % D == 1)
+			iteration(k, preB, lenB, rs);
+		else if constexpr (D == 3)
+			iteration(k, preC, lenC, rs);
+	};
+	if constexpr (D == 2) {
+		uint32_t k = 0;
+		for (; k + 1 < iters; k += 2) {
+			iteration(k, preA, lenA, stA);
+			iteration(k + 1, preB, lenB, LAG == 2 ? stB : stA);
+		}
+		if (k < iters)
+			iteration(k, preA, lenA, stA);
+	} else {
+		// whole bodies unguarded (exact wait counts), then the rest guarded
+		uint32_t k = 0;
+		for (; k + U <= iters; k += U) {
+			one(k, std::integral_constant<uint32_t, 0>{});
+			one(k + 1, std::integral_constant<uint32_t, 1>{});
+			one(k + 2, std::integral_constant<uint32_t, 2>{});
+			if constexpr (U > 3) {
+				one(k + 3, std::integral_constant<uint32_t, 3 % U>{});
+				one(k + 4, std::integral_constant<uint32_t, 4 % U>{});
+				one(k + 5, std::integral_constant<uint32_t, 5 % U>{});
+			}
+		}
+		for (uint32_t u = 0; k < iters; k++, u++) {   // (u < U)
+			if (u == 0)
+				one(k, std::integral_constant<uint32_t, 0>{});
+			else if (u == 1)
+				one(k, std::integral_constant<uint32_t, 1>{});
+			else if (u == 2)
+				one(k, std::integral_constant<uint32_t, 2>{});
+			else if constexpr (U > 3) {
+				if (u == 3)
+					one(k, std::integral_constant<uint32_t, 3 % U>{});
+				else if (u == 4)
+					one(k, std::integral_constant<uint32_t, 4 % U>{});
+			}
+		}
 	}
-	if (k < iters)
-		iteration(k, preA, lenA, stA);
 
 	if (dg & 2048)
 		ndef = 0;
