@@ -88,6 +88,13 @@ struct xfg_open_opts {
 	 * live IPv4 lookup direction, the same flags on every device): 0 =>
 	 * default (2^18), UINT32_MAX => never.  Results never depend on it. */
 	uint32_t qt_min_keys;
+	/* Header window of the pipelined kernels for fixed-stride batches
+	 * whose stride exceeds 64 bytes: 0 => 64 (default: half the bytes of
+	 * a 128-byte window per frame; a frame whose parse reaches past byte
+	 * 64 -- IPv6/TCP, long IPv6 extension chains, IPv4 options -- takes the
+	 * deferred walk over the whole frame), 128 => 128-byte windows.
+	 * Results never depend on it. */
+	uint32_t window;
 };
 
 /*

@@ -110,7 +110,8 @@ def test_c4_imix_1536_stride(G):
 def test_c5_16m_rules_1514b_device_and_host(G):
     rules, v4, v6, ports = config_rules(5, 15_000_000, 1_000_000, 1024)
     data, lens = X.gen_workload(5, 5, 1 << 18, 1536, v4=v4, v6=v6, ports=ports)
-    # (the quotient index of 2^21 buckets: u32 hit-log entries, eight count
-    # passes; the IPv6 frames through the deferred path)
+    # (the quotient index of 2^21 buckets -- more slots than packets here, so
+    # its hits count through the LDS cache and atomics, no hit log -- and
+    # the IPv6 frames through the deferred-packet kernel)
     check(G, "xdpfilt_dny_all", rules, data, lens, 1536, host=True, path=5,
           ipv4_capacity=15_000_000, ipv6_capacity=1_000_000)

@@ -13,7 +13,11 @@ stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
     rule's hits in one workgroup (~1.9M over the grid) overfill that
     workgroup's slice of the rule's partition several times over: the
     spill path (log_counter: straight to the canonical counter, beside the
-    logged entries that reach the QT-order counters) runs at scale.
+    logged entries that reach the QT-order counters) runs at scale;
+  * 9M IPv4 rules at 2^25 packets: an index of 2^21 buckets whose hit log
+    holds u32 local indices (past 65536 per partition) and takes the count
+    kernel eight passes -- the log runs only for batches of at least as many
+    packets as the index has slots (xfg_ctx.c launch_batch).
 """
 import os
 
@@ -52,10 +56,10 @@ def _c3_rules():
     return rules, v4, ports
 
 
-def _check(G, rules, data, lens):
+def _check(G, rules, data, lens, cap=1_000_000):
     ov, orules, ost = X.run_oracle(X.VARIANT_FEATURES["xdpfilt_dny_all"], data, lens, rules,
                                    stride=64, nthreads=_threads())
-    f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=1_000_000)
+    f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=cap)
     f.load_rules(rules)
     v = f.run(data, lens, stride=64)
     assert f.last_path() == f.PATH_QT   # the quotient index (1M dst rules)
@@ -94,3 +98,16 @@ def test_c3_skewed_hits_overfill_log_partitions_2p25(G):
         assert (hits // grid > 2 * pcap).all(), (grid, hits, pcap)
     # (the other rules only see random addresses that happen to be ruled)
     assert int((orules.v4_vals[8:] >> 6).sum()) < n // 1000
+
+
+@pytest.mark.timeout(900)
+def test_wide_hit_log_9m_rules_2p25(G):
+    n4 = 9_000_000
+    v4 = X.rand_keys(41, int(n4 * 1.02) + 16, 4)[:n4]
+    rules = X.RuleSet()
+    rules.v4_keys = v4
+    rules.v4_vals = np.full(len(v4), 2, np.uint64)
+    n = 1 << 25
+    data, lens = X.gen_workload(42, 3, n, 64, v4=v4, dst_permille=600, bad_permille=10)
+    ov, _ = _check(G, rules, data, lens.astype(np.uint16), cap=n4)
+    assert (ov == 2).sum() > n // 3

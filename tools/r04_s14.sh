@@ -6,7 +6,7 @@ step() {
 	local t=$1; shift
 	timeout -k 10 "$t" "$@"
 	local rc=$?
-	case $rc in 124|134|137|139) echo "STOP: rc=$rc from: $*"; exit $rc ;; esac
+	if [ $rc -eq 124 ] || [ $rc -gt 128 ]; then echo "STOP: rc=$rc from: $*"; exit $rc; fi
 	return $rc
 }
 step 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/test_gpu_qt.py tests/test_gpu_configs.py tests/test_a0_gpu_multirank.py tests/test_gpu_io.py > gpurun_out/pytest_s14.log 2>&1

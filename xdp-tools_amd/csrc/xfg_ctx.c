@@ -114,6 +114,8 @@ struct xfg_dev {
 	int lock_ok;
 	uint32_t *defer;                /* pipelined kernel: deferred-packet lists */
 	uint64_t defer_bytes;
+	uint32_t *defer_n;              /* ... their fills (xfg_defer_kernel) */
+	uint64_t defer_n_bytes;
 	uint32_t *tlog, *pfill;         /* hit log: wave regions, slice fills */
 	uint16_t *pbuf;                 /* hit log: partition slices */
 	uint64_t tlog_bytes, pbuf_bytes, pfill_bytes;
@@ -149,6 +151,7 @@ struct xfg_ctx {
 	int qt_dirty;
 	uint32_t qt_gen;
 	uint32_t qt_min_keys;
+	uint32_t window;                /* header window above a 64-byte stride: 64 or 128 */
 	uint32_t port_flag_cnt[8];
 	/* multi-process reduction */
 	ncclComm_t comm;
@@ -386,6 +389,7 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->fb_dl);
 	hipFree(d->fb_dv);
 	hipFree(d->defer);
+	hipFree(d->defer_n);
 	hipFree(d->tlog);
 	hipFree(d->pbuf);
 	hipFree(d->rec);
@@ -479,6 +483,14 @@ int xfg_open(xfg_ctx **out, const struct xfg_open_opts *opts)
 	ctx->qt_min_keys = XFG_QT_MIN_KEYS;
 	if (opts->sz >= offsetof(struct xfg_open_opts, qt_min_keys) + sizeof(uint32_t) && opts->qt_min_keys)
 		ctx->qt_min_keys = opts->qt_min_keys;
+	ctx->window = 64;
+	if (opts->sz >= offsetof(struct xfg_open_opts, window) + sizeof(uint32_t) && opts->window) {
+		if (opts->window != 64 && opts->window != 128) {
+			err = -EINVAL;
+			goto fail;
+		}
+		ctx->window = opts->window;
+	}
 	uint32_t cap4 = opts->ipv4_capacity ? opts->ipv4_capacity : XFG_DEFAULT_MAP_CAPACITY;
 	uint32_t cap6 = opts->ipv6_capacity ? opts->ipv6_capacity : XFG_DEFAULT_MAP_CAPACITY;
 	uint32_t cape = opts->eth_capacity ? opts->eth_capacity : XFG_DEFAULT_MAP_CAPACITY;
@@ -1370,14 +1382,19 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	a->stride = b->stride;
 	a->lens_u16 = b->lens_u16;
 	a->verdicts = verdicts;
-	/* Header window: the fixed-stride 64-byte layout needs no more than its
-	 * stride; everything else stages 128 bytes (every synthetic class and all
-	 * common headers parse within 78 bytes; a longer parse reads HBM). */
-	a->window = (!b->offsets && b->stride && b->stride <= 64) ? 64 : 128;
+	/* Header window: 64 bytes for fixed strides (a parse that reaches past
+	 * it -- IPv6/TCP's doff at byte 66, long IPv6 extension chains -- is a
+	 * deferred walk over the frame in HBM), unless the context asked for
+	 * 128 (xfg_open_opts.window: such frames then stay on the fast path);
+	 * frames at offsets stage 128 bytes in the general kernel.  On C4/C5's
+	 * 1536-byte slots the 64-byte window was 14 % faster (r04 session 16). */
+	a->window = (!b->offsets && b->stride && (b->stride <= 64 || ctx->window == 64)) ? 64 : 128;
 #ifdef XFG_DIAG
-	const char *wn = getenv("XFG_WINDOW");   /* "64": 64-byte windows at any stride */
-	if (wn && !strcmp(wn, "64"))
+	const char *wn = getenv("XFG_WINDOW");   /* "64" / "128" above a 64-byte stride */
+	if (wn && !strcmp(wn, "64") && !b->offsets && b->stride)
 		a->window = 64;
+	else if (wn && !strcmp(wn, "128") && b->stride > 64)
+		a->window = 128;
 #endif
 	/* The pipelined kernel takes every fixed-stride batch whose windows can
 	 * be loaded without a length (stride >= window, 16-byte aligned; packet
@@ -1479,10 +1496,13 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	int err = 0;
 	struct xfg_kargs a = *a0;
 	const char *cm = NULL;
+	int nolog = 0;   /* (diagnostics: every kernel without the hit log) */
 #ifdef XFG_DIAG
 	cm = getenv("XFG_COUNT");   /* diagnostics build only: "atomic" */
 	if (cm && !strcmp(cm, "atomic"))
-		a.qt = NULL;             /* (the QT kernel counts through the hit log only) */
+		a.qt = NULL;             /* (the QT kernel's counting is the log, or no log) */
+	const char *lg = getenv("XFG_LOG");   /* "off": counters by LDS cache + atomics */
+	nolog = lg && !strcmp(lg, "off");
 #endif
 	/* small rule sets: a direct LDS counter per hash-map slot (their few
 	 * counters are hot: more than the LDS counter cache holds) */
@@ -1505,7 +1525,13 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * through a handful of overfull partitions to contended atomics) */
 	const uint64_t nkeys = (uint64_t)a.t4.count + a.t6.count + a.te.count;
 	const int logged = nkeys > XFG_LOG_MIN_KEYS;
-	const int log_off = !a.pipe || !logged || a.dcnt >= a.gbase[3] || (cm && !strcmp(cm, "atomic"));
+	const int log_no = !a.pipe || !logged || a.dcnt >= a.gbase[3] || (cm && !strcmp(cm, "atomic"));
+	/* (a batch of fewer packets than counters: the count kernel's pass over
+	 * every counter costs more than the atomics it saves -- C5's 15M + 1M
+	 * rules at 2^23 packets: 0.45 ms with atomics, 0.65-0.71 with the log;
+	 * C4's 1M at 2^23 and C3's at 2^24 and 2^26 keep the log, r04 sessions
+	 * 16 and 18) */
+	int qt_nolog = 0;
 	if (a.qt) {
 		const int k5 = 5, wi5 = a.window > 64;
 		const int pc = d->occ[k5][wi5][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
@@ -1513,9 +1539,16 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		uint64_t g5 = (uint64_t)d->ncu * (pc > 0 ? pc : 1), need5 = (a.n + pw - 1) / pw;
 		if (g5 > need5)
 			g5 = need5 ? need5 : 1;
-		if (log_off || g5 > XFG_LOG_SLICES_MAX || !qt_log_fits(d->qt_n, d->qt_live == 3))
+		/* (a log the count kernel cannot take: the index kernel counts
+		 * through its LDS counter cache and atomics instead) */
+		if (log_no)
 			a.qt = NULL;
+		else if (nolog || g5 > XFG_LOG_SLICES_MAX || !qt_log_fits(d->qt_n, d->qt_live == 3) ||
+			 (uint64_t)d->qt_n > a.n)
+			qt_nolog = 1;
 	}
+	const int log_off = log_no || nolog ||
+			    (!a.qt && (uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES > a.n);
 	if (!a.qt && a.v6d) {   /* (the IPv6 keys need the general kernel then) */
 		a.km = 0;
 		a.v6d = 0;
@@ -1580,6 +1613,22 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			goto out;
 		a.defer = d->defer;
 		a.defer_cap = (uint32_t)cap;
+		/* the quotient-index kernel lists its deferred packets for
+		 * xfg_defer_kernel (two workgroups a CU over every list) */
+		int sep = kind == 5 && nw <= XFG_DEFER_SRC_MAX;
+#ifdef XFG_DIAG
+		const char *dfe = getenv("XFG_DEFER");   /* "inline": each wave's own tail */
+		if (dfe && !strcmp(dfe, "inline"))
+			sep = 0;
+#endif
+		if (sep) {
+			if ((err = scratch(d, (void **)&d->defer_n, &d->defer_n_bytes, nw * 4)))
+				goto out;
+			a.defer_n = d->defer_n;
+			a.defer_nsrc = (uint32_t)nw;
+			a.defer_sep = 1;
+			a.defer_grid = (uint32_t)d->ncu * 2;
+		}
 	}
 	/* hit log (pipelined kernels): the hash-map counters without a direct
 	 * LDS counter, when the count kernel's histogram covers them; the wave
@@ -1591,7 +1640,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	/* (a range past one histogram: the count kernel takes it in passes; past
 	 * 65536 local indices the slices hold u32) */
 	const int pwide = hist > 65536;
-	if (!log_off && hist <= (uint64_t)XFG_LOG_HIST_MAX * XFG_LOG_PASSES_MAX &&
+	if (!log_off && !qt_nolog && hist <= (uint64_t)XFG_LOG_HIST_MAX * XFG_LOG_PASSES_MAX &&
 	    grid <= XFG_LOG_SLICES_MAX) {
 		/* slice (partition, workgroup): twice a uniform share of the
 		 * most the workgroup's waves can log (a fuller one spills) */
@@ -1615,7 +1664,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.log_span = (uint32_t)hist;
 		a.pwide = (uint32_t)pwide;
 	}
-	if (a.qt && !a.pbuf) {   /* (decided above: cannot happen) */
+	if (a.qt && !a.pbuf && !qt_nolog) {   /* (decided above: cannot happen) */
 		err = -EIO;
 		goto out;
 	}

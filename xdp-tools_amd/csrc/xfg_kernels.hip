@@ -1368,6 +1368,108 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	}
 }
 
+// ---------------------------------------------------------------- deferred packets
+// The quotient-index kernel's deferred packets (kargs.defer_sep): every
+// wave's list (a.defer + w * defer_cap, a.defer_n[w] entries, defer_nsrc
+// lists), classified by the whole reference walk (classify_staged), one
+// packet per lane, the lists' concatenation dealt round-robin over the grid:
+// the dependent loads of a few hundred thousand walks overlap across the chip
+// instead of running as each classify wave's serial tail.
+constexpr int DF_THREADS = 256;
+constexpr uint32_t DF_SRC_MAX = XFG_DEFER_SRC_MAX;   // source lists (classify waves)
+
+template <uint32_t FEAT, int W>
+__global__ __launch_bounds__(DF_THREADS) void xfg_defer_kernel(const xfg_kargs a)
+{
+	constexpr int ROWDW = Pkt<W>::ROWDW;
+	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
+	constexpr uint32_t CH = DF_SRC_MAX / DF_THREADS;
+	__shared__ uint32_t win[DF_THREADS * ROWDW];
+	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
+	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
+	__shared__ uint32_t s_pre[DF_SRC_MAX + 1], s_part[DF_THREADS];
+	__shared__ unsigned long long s_stats[6];
+	extern __shared__ uint32_t s_dyn[];
+	const int tid = threadIdx.x, lane = tid & 63;
+	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
+	cn.init(a, tid, DF_THREADS);
+	if (tid < 6)
+		s_stats[tid] = 0;
+	const uint32_t *s_ports = stage_ports<FEAT>(a, s_tab, s_dyn, tid, DF_THREADS);
+	// exclusive prefix sums of the lists' fills: CH per thread, then the
+	// DF_THREADS partial sums by one wave
+	const uint32_t ns = a.defer_nsrc;
+	uint32_t v[CH], sum = 0;
+#pragma unroll
+	for (uint32_t j = 0; j < CH; j++) {
+		const uint32_t w = tid * CH + j;
+		v[j] = w < ns ? a.defer_n[w] : 0u;
+		sum += v[j];
+	}
+	s_part[tid] = sum;
+	__syncthreads();
+	if (tid < 64) {
+		uint32_t p[DF_THREADS / 64], t = 0;
+#pragma unroll
+		for (int j = 0; j < DF_THREADS / 64; j++) {
+			p[j] = s_part[tid * (DF_THREADS / 64) + j];
+			t += p[j];
+		}
+		uint32_t x = t;   // inclusive scan over the wave
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t y = __shfl_up(x, o);
+			if (lane >= o)
+				x += y;
+		}
+		x -= t;
+#pragma unroll
+		for (int j = 0; j < DF_THREADS / 64; j++) {
+			s_part[tid * (DF_THREADS / 64) + j] = x;
+			x += p[j];
+		}
+	}
+	__syncthreads();
+	uint32_t run = s_part[tid];
+#pragma unroll
+	for (uint32_t j = 0; j < CH; j++) {
+		s_pre[tid * CH + j] = run;
+		run += v[j];
+	}
+	if (tid == DF_THREADS - 1)
+		s_pre[DF_SRC_MAX] = run;
+	__syncthreads();
+	const uint32_t total = s_pre[DF_SRC_MAX];
+	LaneStats st;
+	for (uint32_t base = blockIdx.x * DF_THREADS; base < total; base += gridDim.x * DF_THREADS) {
+		const uint32_t q = base + tid;
+		const bool ok = q < total;
+		uint32_t gi = 0, len = 0, tag = CT_NONE;
+		if (ok) {
+			uint32_t lo = 0, hi = DF_SRC_MAX;   // the list: last w with s_pre[w] <= q
+			while (hi - lo > 1) {
+				const uint32_t mid = (lo + hi) >> 1;
+				if (s_pre[mid] <= q)
+					lo = mid;
+				else
+					hi = mid;
+			}
+			gi = a.defer[(uint64_t)lo * a.defer_cap + (q - s_pre[lo])];
+			len = min(load_len(a, gi), a.stride);
+		}
+		const uint32_t act = classify_staged<FEAT, W>(a, s_ports, &win[tid * ROWDW], ok, gi, len, tag);
+		if (ok)
+			__builtin_nontemporal_store((uint8_t)act, a.verdicts + gi);
+		cn.bump(a, tag, lane);
+		st.add(act, len);
+	}
+	st.reduce(s_stats, lane);
+	__syncthreads();
+	if (tid < 6 && s_stats[tid])
+		atomicAdd(&a.stats[tid], s_stats[tid]);
+	cn.flush(a, tid, DF_THREADS);
+}
+
 template <uint32_t FEAT, bool L16, bool BOTH, bool WIDE>
 void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
@@ -1379,6 +1481,12 @@ void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 	else
 		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+	if (a.defer_sep) {
+		if (a.window <= 64)
+			hipLaunchKernelGGL((xfg_defer_kernel<FEAT, 64>), dim3(a.defer_grid), dim3(DF_THREADS), dl, s, a);
+		else
+			hipLaunchKernelGGL((xfg_defer_kernel<FEAT, 128>), dim3(a.defer_grid), dim3(DF_THREADS), dl, s, a);
+	}
 }
 
 // (qt_live 3: both IPv4 lookups through the index; pwide: an index past

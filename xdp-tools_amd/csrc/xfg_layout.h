@@ -97,6 +97,7 @@
 #define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
 #define XFG_LOG_PASSES_MAX 32u    /* histogram passes per partition (span 512K) */
 #define XFG_LOG_SLICES_MAX 1024u  /* slices per partition: classify workgroups */
+#define XFG_DEFER_SRC_MAX 4096u   /* deferred lists (classify waves) xfg_defer_kernel takes */
 #define XFG_LOG_MIN_KEYS  256u    /* fewer hash-map keys: LDS counter cache, no log */
 
 
@@ -175,9 +176,17 @@ struct xfg_kargs {
 	 * partition and pass); past 65536 the slices hold u32 indices (pwide) */
 	uint32_t log_span;
 	uint32_t pwide;
-	/* Pipelined kernel: deferred packets, defer_cap entries per wave */
+	/* Pipelined kernel: deferred packets, defer_cap entries per wave.  With
+	 * defer_sep the quotient-index kernel only lists them (its fill per wave
+	 * in defer_n, defer_nsrc waves) and xfg_defer_kernel, defer_grid
+	 * workgroups, classifies them after it, spread over the whole chip
+	 * instead of each wave's serial tail */
 	uint32_t *defer;
 	uint32_t defer_cap;
+	uint32_t *defer_n;
+	uint32_t defer_nsrc;
+	uint32_t defer_sep;
+	uint32_t defer_grid;
 	uint32_t diag;                /* diagnostics build only (XFG_DIAG_MASK); 0 */
 	/* Header-window batches (xfg_classify_host): each slot holds only the
 	 * first `stride` bytes of its frame, lens are the frames' true lengths.

@@ -46,6 +46,12 @@
 #ifndef XFG_QT_DEPTH     /* tiles of windows in flight per wave (3: with XFG_QT_LAG 2 only) */
 #define XFG_QT_DEPTH 2
 #endif
+#ifndef XFG_QT_NTLEN     /* lengths loaded non-temporal (A/B) */
+#define XFG_QT_NTLEN 0
+#endif
+#ifndef XFG_QT_NTLOG     /* hit-log stores non-temporal (A/B) */
+#define XFG_QT_NTLOG 0
+#endif
 #ifndef XFG_QT_WC_R      /* ring entries per partition, 64-byte windows */
 #define XFG_QT_WC_R 128
 #endif
@@ -127,6 +133,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const uint64_t qb2 = BOTH ? rfl64((uint64_t)(uintptr_t)a.qt2) : 0;
 	const uint32_t qbase2 = BOTH ? rfl(a.qt_base) : 0u;
 	const bool klive = a.t4.count != 0;
+	// (no hit log -- an index too large for the count kernel to pay, the
+	// host's choice: every hit through the LDS counter cache or an atomic)
+	const bool logon = a.pbuf != nullptr;
 	// (IPv6 keys live, no Ethernet key: every IPv6 frame takes the deferred
 	// path -- the whole reference walk over the canonical tables)
 	const bool v6d = (FEAT & F_IPV6) != 0 && a.v6d != 0;
@@ -159,9 +168,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	uint32_t *const dlist = reinterpret_cast<uint32_t *>(
 		rfl64((uint64_t)(uintptr_t)(a.defer + ((uint64_t)blockIdx.x * NW + wv) * a.defer_cap)));
 	uint32_t tn = 0;
-	// a hit's counter: a QT slot to the hit log (the host runs this kernel
-	// only with the log on); a ruled port's to its table slot's LDS
-	// counter; any other (the deferred packets') through Counters::bump
+	// a hit's counter: a QT slot to the hit log (without one, to the LDS
+	// counter cache or an atomic on its QT-order count); a ruled port's to
+	// its table slot's LDS counter; any other (the deferred packets')
+	// through Counters::bump
 	auto count = [&](uint32_t tag, uint32_t pslot) {
 		const bool q = (tag != CT_NONE) & ((tag & QTAG) != 0);
 		const bool ps = pslot < XFG_PORT_TAB;
@@ -172,17 +182,22 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				atomicAdd(reinterpret_cast<uint32_t *>(a.pbuf) + qs, 1u);
 		} else {
 			if (q) {
-				const uint32_t p = log_part(qs);
-				const uint32_t r = atomicAdd(&s_res[p], 1u);
-				if (r < WR) {
-					const uint32_t t = atomicAdd(&s_hd[2 * p], 1u);
-					s_ring[p * WR + (t & (WR - 1))] = (ring_t)log_local(qs);
-					atomicAdd(&s_hd[2 * p + 1], 1u);
-				} else {   // the ring is full: the LDS counter cache
-					atomicSub(&s_res[p], 1u);
-					if (!cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
-						atomicAdd(a.qt_hits + qs, 1ull);
+				bool ring = false;
+				if (logon) {
+					const uint32_t p = log_part(qs);
+					const uint32_t r = atomicAdd(&s_res[p], 1u);
+					ring = r < WR;
+					if (ring) {
+						const uint32_t t = atomicAdd(&s_hd[2 * p], 1u);
+						s_ring[p * WR + (t & (WR - 1))] = (ring_t)log_local(qs);
+						atomicAdd(&s_hd[2 * p + 1], 1u);
+					} else {
+						atomicSub(&s_res[p], 1u);
+					}
 				}
+				// the ring full (or no log): the LDS counter cache
+				if (!ring && !cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
+					atomicAdd(a.qt_hits + qs, 1ull);
 			}
 		}
 		if constexpr (PORTS)
@@ -199,10 +214,15 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		for (uint32_t o = lane; o < cnt; o += 64) {
 			const uint32_t e = s_ring[p * WR + ((fl + o) & (WR - 1))];
 			const uint32_t pos = fl + o;
-			if (pos < a.pcap)
-				*reinterpret_cast<__attribute__((address_space(1))) ring_t *>(
-					(uintptr_t)(reinterpret_cast<ring_t *>(a.pbuf) + p * wc_pstep + wc_slice0 + pos)) = (ring_t)e;
-			else {
+			if (pos < a.pcap) {
+				auto *d = reinterpret_cast<__attribute__((address_space(1))) ring_t *>(
+					(uintptr_t)(reinterpret_cast<ring_t *>(a.pbuf) + p * wc_pstep + wc_slice0 + pos));
+#if XFG_QT_NTLOG   /* (A/B: the hit log's lines stored non-temporal) */
+				__builtin_nontemporal_store((ring_t)e, d);
+#else
+				*d = (ring_t)e;
+#endif
+			} else {
 				const uint32_t g = ((e >> 4) << 12) | (p << 4) | (e & 15);
 				if (!cache_hit(cn.ctag, cn.ccnt, QTAG | g, 1))
 					atomicAdd(a.qt_hits + g, 1ull);
@@ -252,6 +272,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr uint32_t lsh = L16 ? 1u : 2u;
 	typedef typename std::conditional<L16, uint16_t, uint32_t>::type len_t;
 	const uint64_t lb = rfl64((uint64_t)(uintptr_t)a.lens);
+	auto ld_len = [](uint64_t p) {
+		const auto *q = reinterpret_cast<const __attribute__((address_space(1))) len_t *>(p);
+#if XFG_QT_NTLEN   /* (A/B: the lengths streamed like the windows) */
+		return __builtin_nontemporal_load(q);
+#else
+		return *q;
+#endif
+	};
 	// (a whole tile -- every one but a ragged last -- takes a uniform branch
 	// with no per-lane clamps: a scalar tile base and per-lane offsets that
 	// do not change from tile to tile; the same loads either way)
@@ -268,8 +296,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 							 : reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
 				pre[it] = __builtin_nontemporal_load(src);
 			}
-			plen = *reinterpret_cast<const __attribute__((address_space(1))) len_t *>(
-				lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
+			plen = ld_len(lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
 		} else {
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
@@ -280,7 +307,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				pre[it] = __builtin_nontemporal_load(src);
 			}
 			const uint64_t la = lb + ((uint64_t)(base + ((uint32_t)lane < rem ? lane : 0u)) << lsh);
-			plen = *reinterpret_cast<const __attribute__((address_space(1))) len_t *>(la);
+			plen = ld_len(la);
 		}
 	};
 
@@ -434,7 +461,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
-		if (vW)
+		if (vW && logon)
 			wc_flush();
 
 		PMARK("S");
@@ -627,7 +654,13 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	if (dg & 2048)
 		ndef = 0;
 	// the deferred packets: the whole reference walk over the canonical
-	// table (classify_staged), 64 at a time
+	// table (classify_staged), 64 at a time -- or listed for
+	// xfg_defer_kernel, which takes every wave's list after this kernel
+	if (a.defer_sep) {
+		if (lane == 0)
+			a.defer_n[blockIdx.x * NW + wv] = ndef;
+		ndef = 0;
+	}
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
 		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
 		const bool ok = d0 + lane < ndef;

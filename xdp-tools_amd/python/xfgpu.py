@@ -68,7 +68,7 @@ class OpenOpts(C.Structure):
                 ("devices", C.POINTER(C.c_int)), ("ndev", C.c_int),
                 ("ipv4_capacity", C.c_uint32), ("ipv6_capacity", C.c_uint32),
                 ("eth_capacity", C.c_uint32), ("hash_seed", C.c_uint32),
-                ("qt_min_keys", C.c_uint32)]
+                ("qt_min_keys", C.c_uint32), ("window", C.c_uint32)]
 
 
 class Batch(C.Structure):
@@ -262,7 +262,8 @@ class Filter:
     """One xfg context: a selected xdpfilt_* program, its maps, and devices."""
 
     def __init__(self, features=FEAT_ALL | FEAT_DENY, devices=None, ndev=None,
-                 ipv4_capacity=0, ipv6_capacity=0, eth_capacity=0, hash_seed=0, qt_min_keys=0):
+                 ipv4_capacity=0, ipv6_capacity=0, eth_capacity=0, hash_seed=0, qt_min_keys=0,
+                 window=0):
         opts = OpenOpts()
         opts.sz = C.sizeof(OpenOpts)
         opts.features = features
@@ -278,6 +279,7 @@ class Filter:
         opts.eth_capacity = eth_capacity
         opts.hash_seed = hash_seed
         opts.qt_min_keys = qt_min_keys
+        opts.window = window
         ctx = C.c_void_p()
         _check(lib.xfg_open(C.byref(ctx), C.byref(opts)), "xfg_open")
         self.ctx = ctx
