@@ -12,8 +12,9 @@ stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
   * a skewed C3 at 2^25: every hit on one of 8 hot rules, so each hot
     rule's hits in one workgroup (~1.9M over the grid) overfill that
     workgroup's slice of the rule's partition several times over: the
-    spill path (log_counter: straight to the canonical counter, beside the
-    logged entries that reach the QT-order counters) runs at scale;
+    spill paths (a full LDS ring or a chunk past the slice: the LDS counter
+    cache, then an atomic on the QT-order count, beside the logged entries
+    the count kernel adds) run at scale;
   * 9M IPv4 rules at 2^25 packets: an index of 2^21 buckets whose hit log
     holds u32 local indices (past 65536 per partition) and takes the count
     kernel eight passes -- the log runs only for batches of at least as many

@@ -1613,13 +1613,14 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			goto out;
 		a.defer = d->defer;
 		a.defer_cap = (uint32_t)cap;
-		/* the quotient-index kernel lists its deferred packets for
-		 * xfg_defer_kernel (two workgroups a CU over every list) */
-		int sep = kind == 5 && nw <= XFG_DEFER_SRC_MAX;
+		/* (diagnostics: the quotient-index kernel lists its deferred
+		 * packets for xfg_defer_kernel, two workgroups a CU over every
+		 * list -- 1-3 % slower than each wave's own tail on C3 and C5,
+		 * r04 session 19) */
+		int sep = 0;
 #ifdef XFG_DIAG
-		const char *dfe = getenv("XFG_DEFER");   /* "inline": each wave's own tail */
-		if (dfe && !strcmp(dfe, "inline"))
-			sep = 0;
+		const char *dfe = getenv("XFG_DEFER");   /* "kernel" */
+		sep = dfe && !strcmp(dfe, "kernel") && kind == 5 && nw <= XFG_DEFER_SRC_MAX;
 #endif
 		if (sep) {
 			if ((err = scratch(d, (void **)&d->defer_n, &d->defer_n_bytes, nw * 4)))

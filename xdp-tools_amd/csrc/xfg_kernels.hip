@@ -1368,6 +1368,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	}
 }
 
+#ifdef XFG_DIAG   // (1-3 % slower than each wave's tail: DESIGN.md §5.3; diagnostics only)
 // ---------------------------------------------------------------- deferred packets
 // The quotient-index kernel's deferred packets (kargs.defer_sep): every
 // wave's list (a.defer + w * defer_cap, a.defer_n[w] entries, defer_nsrc
@@ -1469,6 +1470,7 @@ __global__ __launch_bounds__(DF_THREADS) void xfg_defer_kernel(const xfg_kargs a
 		atomicAdd(&a.stats[tid], s_stats[tid]);
 	cn.flush(a, tid, DF_THREADS);
 }
+#endif
 
 template <uint32_t FEAT, bool L16, bool BOTH, bool WIDE>
 void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
@@ -1481,12 +1483,14 @@ void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 	else
 		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+#ifdef XFG_DIAG
 	if (a.defer_sep) {
 		if (a.window <= 64)
 			hipLaunchKernelGGL((xfg_defer_kernel<FEAT, 64>), dim3(a.defer_grid), dim3(DF_THREADS), dl, s, a);
 		else
 			hipLaunchKernelGGL((xfg_defer_kernel<FEAT, 128>), dim3(a.defer_grid), dim3(DF_THREADS), dl, s, a);
 	}
+#endif
 }
 
 // (qt_live 3: both IPv4 lookups through the index; pwide: an index past

@@ -46,6 +46,9 @@
 #ifndef XFG_QT_DEPTH     /* tiles of windows in flight per wave (3: with XFG_QT_LAG 2 only) */
 #define XFG_QT_DEPTH 2
 #endif
+#ifndef XFG_QT_SPEC      /* both directions: src buckets loaded with the dst ones (A/B) */
+#define XFG_QT_SPEC 0
+#endif
 #ifndef XFG_QT_NTLEN     /* lengths loaded non-temporal (A/B) */
 #define XFG_QT_NTLEN 0
 #endif
@@ -79,6 +82,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// (both directions: the src buckets loaded in R are matched the next
 	// iteration, so a third tile of windows could not stay in flight)
 	constexpr uint32_t D = BOTH ? 2u : XFG_QT_DEPTH;
+	// (both directions: the src buckets loaded in R for the packets whose dst
+	// lookup decided nothing, matched by R2 an iteration later -- or, SPEC,
+	// loaded beside the dst buckets in L for every IPv4 packet and matched
+	// in R with them)
+	constexpr bool SPEC = BOTH && XFG_QT_SPEC;
+	constexpr bool R2 = BOTH && !SPEC;
 	static_assert(D == 2 || (D == 3 && LAG == 2), "window depth: 2, or 3 with a bucket lag of 2");
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	constexpr uint32_t QTAG = CT_QTAG;   // tag bit: a QT slot (hit log), not a counter identity
@@ -322,9 +331,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	struct RSt {
 		uint32_t key, b, pk, tag, key2, b2;
 		bool sel;
-		u32x4 bk0, bk1;
+		u32x4 bk0, bk1, cs0, cs1;
 	};
-	RSt stA = { 0, 0, pk3(A_NONE, XFG_PORT_TAB, 0), CT_NONE, 0, 0, false, { 0, 0, 0, 0 }, { 0, 0, 0, 0 } };
+	RSt stA = { 0, 0, pk3(A_NONE, XFG_PORT_TAB, 0), CT_NONE, 0, 0, false, { 0, 0, 0, 0 }, { 0, 0, 0, 0 },
+		    { 0, 0, 0, 0 }, { 0, 0, 0, 0 } };
 	RSt stB = stA;
 	// (both directions: the src key's entry and bucket from P; tile k-1's
 	// state after its dst lookup, for R2 next iteration; its src bucket)
@@ -375,8 +385,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// (both directions: W works on tile k-2, whose src lookup -- read
 		// last iteration for the packets whose dst lookup decided nothing --
 		// R2 resolves first; one directions: W works on tile k-1)
-		const bool vW = BOTH ? (k >= LAG + 1 && tP - (LAG + 1) * step < nt) : vR;
-		if constexpr (BOTH) {
+		const bool vW = R2 ? (k >= LAG + 1 && tP - (LAG + 1) * step < nt) : vR;
+		if constexpr (R2) {
 			PMARK("R2");
 			// lookup_verdict_ipv4 (xdpfilt_prog.h:121-134): the src key
 			// only when the dst key decided nothing -- the first matching
@@ -412,7 +422,17 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const uint32_t x_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
 			const uint32_t x_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, rs.tag));
 			const uint32_t x_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
-			if constexpr (BOTH) {   // to R2 next iteration
+			if constexpr (SPEC) {   // the src lookup, its bucket loaded beside the dst one
+				const bool need = rs.sel & !found & !defer;
+				bool f2;
+				uint32_t ix2;
+				const bool ovf2 = match(rs.cs0, rs.cs1, rs.key2, f2, ix2);
+				f2 &= need;
+				const bool d2 = need & !f2 & ovf2;
+				w_act = pick(f2, HIT, pick(d2, A_DEFER, x_act));
+				w_tag = pick(f2, QTAG | (qbase2 + rs.b2 * XFG_QT_SLOTS + ix2), pick(d2, CT_NONE, x_tag));
+				w_ps = pick(f2 | d2, XFG_PORT_TAB, x_ps);
+			} else if constexpr (R2) {   // to R2 next iteration
 				q_need = rs.sel & !found & !defer;
 				q_act = x_act;
 				q_tag = x_tag;
@@ -425,14 +445,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				w_tag = x_tag;
 				w_ps = x_ps;
 			}
-		} else if constexpr (BOTH) {
+		} else if constexpr (R2) {
 			q_need = false;
 			q_act = A_NONE;
 			q_tag = CT_NONE;
 			q_ps = XFG_PORT_TAB;
 			q_b2 = 0;
 		}
-		if constexpr (BOTH) {
+		if constexpr (R2) {
 			// tile k-1's src buckets (bucket 0 for a packet whose dst lookup
 			// decided it: a shared line), as L loads (see there)
 			if (!(dg & 2)) {
@@ -446,7 +466,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		PMARK("W");
 		// ---- W: verdicts, counters, stats, deferrals of tile k-1 (k-2)
 		if (vW) {
-			const uint32_t gi = (tP - (LAG + (BOTH ? 1 : 0)) * step) * 64 + lane;
+			const uint32_t gi = (tP - (LAG + (R2 ? 1 : 0)) * step) * 64 + lane;
 			if (w_act <= A_PASS && !(dg & 8)) {
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
 			}
@@ -502,20 +522,29 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// looked up once); R moves them to the packet's lane.  Every lane
 		// loads (a fixed count); one whose frame is not IPv4 loads bucket 0
 		// (a shared line).
-		uint32_t hk = 0, lbk = 0, hk2 = 0;
+		uint32_t hk = 0, lbk = 0, hk2 = 0, lbk2 = 0;
 		if (vP) {
 			const uint32_t e3 = myrow[3], e6 = myrow[6], e7 = myrow[7], e8 = myrow[8];
 			const uint32_t key = dlive ? __builtin_amdgcn_alignbyte(e8, e7, 2) : __builtin_amdgcn_alignbyte(e7, e6, 2);
 			hk = xfg_qt_hash(key, qseed);
-			lbk = pick((e3 & 0xffffu) == 0x0008u, hk >> rsh, 0u);
-			if constexpr (BOTH)   // the src key (saddr, bytes 26..29)
+			const bool ip4 = (e3 & 0xffffu) == 0x0008u;
+			lbk = pick(ip4, hk >> rsh, 0u);
+			if constexpr (BOTH) {   // the src key (saddr, bytes 26..29)
 				hk2 = xfg_qt_hash(__builtin_amdgcn_alignbyte(e7, e6, 2), qseed);
+				lbk2 = pick(ip4, hk2 >> rsh, 0u);
+			}
 		}
 		if (!(dg & 2)) {
 			const auto ab = __builtin_amdgcn_permlane32_swap(lbk, lbk, false, false);
 			const uint64_t hb = qb + (uint64_t)(lane >> 5) * 16;
 			rs.bk0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[0] << 5));
 			rs.bk1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb + ((uint64_t)ab[1] << 5));
+			if constexpr (SPEC) {
+				const auto ab2 = __builtin_amdgcn_permlane32_swap(lbk2, lbk2, false, false);
+				const uint64_t hb2 = qb2 + (uint64_t)(lane >> 5) * 16;
+				rs.cs0 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[0] << 5));
+				rs.cs1 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(hb2 + ((uint64_t)ab2[1] << 5));
+			}
 		}
 		__builtin_amdgcn_sched_barrier(0);
 		PMARK("P");
@@ -600,7 +629,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	}
 	// (one more with both directions: the last tile's src lookup resolves
 	// an iteration after its dst lookup)
-	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 1 + LAG + (BOTH ? 1 : 0) : 0u;
+	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 1 + LAG + (R2 ? 1 : 0) : 0u;
 	// iteration k uses window buffer k % D and state set k % LAG: the loop
 	// body is U = lcm(D, LAG) iterations
 	constexpr uint32_t U = D == 3 ? 3 * LAG : 2;
