@@ -425,23 +425,35 @@ def test_qt_hits_concentrated_in_few_log_partitions(G, stride):
 
 @pytest.mark.parametrize("variant", ["xdpfilt_dny_all", "xdpfilt_alw_all", "xdpfilt_dny_ip"])
 @pytest.mark.parametrize("stride", [64, 128, 1536])
-def test_qt_with_ipv6_rules_defers_ipv6_frames(G, variant, stride):
+@pytest.mark.parametrize("dirs6", ["dst", "src", "both"])
+def test_qt_with_ipv6_rules(G, variant, stride, dirs6):
     """IPv6 rules beside the IPv4 map (C5's shape, no Ethernet rule): the
-    index kernel still takes the batch, every IPv6 frame goes to its
-    deferred path -- the whole walk over the canonical tables (dst then src,
-    xdpfilt_prog.h:152-165) -- and the IPv4 lookups stay on the index."""
+    index kernel still takes the batch and the IPv4 lookups stay on the
+    index.  With one IPv6 direction live (dst or src rules) the kernel looks
+    the IPv6 keys up in its loop -- up to 16 frames a tile through their home
+    bucket lines, the rest and the misses in overflowed buckets deferred;
+    with both live every IPv6 frame takes the deferred walk over the
+    canonical tables (dst then src, xdpfilt_prog.h:152-165)."""
     rng = np.random.default_rng(101)
     rules, v4, ports = one_direction_rules(102, 20000, 2)
     v6 = X.rand_keys(103, 4000, 16)
     rules.v6_keys = v6
-    f6 = np.where(rng.random(len(v6)) < 0.5, 2, 1).astype(np.uint64)   # dst or src rules
+    if dirs6 == "both":
+        f6 = np.where(rng.random(len(v6)) < 0.5, 2, 1).astype(np.uint64)
+    else:
+        f6 = np.full(len(v6), 2 if dirs6 == "dst" else 1, np.uint64)
     f6[rng.random(len(v6)) < 0.1] |= 4
     rules.v6_vals = f6 | (rng.integers(0, 50, len(v6)).astype(np.uint64) << 6)
     kind = 5 if stride == 1536 else 3
     d1, l1 = X.gen_workload(104, kind, 1 << 15, stride, v4=v4, v6=v6, ports=ports)
     d2, l2 = fuzz_at(105, 1 << 14, stride, rules, ports)
-    data = np.concatenate([d1, d2])
-    lens = np.concatenate([l1, l2])
+    # a run of IPv6 frames only: whole tiles with more than 16 IPv6 lookups
+    fr = d1.reshape(-1, stride)
+    six = np.nonzero((fr[:, 12] == 0x86) & (fr[:, 13] == 0xdd))[0]
+    pick = six[np.arange(1 << 13) % len(six)]
+    d3, l3 = fr[pick].reshape(-1), l1[pick]
+    data = np.concatenate([d1, d2, d3])
+    lens = np.concatenate([l1, l2, l3])
     ov = run_both(G, variant, rules, data, lens, stride, ipv6_capacity=1 << 13)
     assert len(np.unique(ov)) == 3
 

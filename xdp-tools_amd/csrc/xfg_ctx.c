@@ -1665,6 +1665,15 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.log_span = (uint32_t)hist;
 		a.pwide = (uint32_t)pwide;
 	}
+	/* IPv6 rules beside the index: their lookups in the kernel's loop when
+	 * exactly one IPv6 direction can hit (else every IPv6 frame deferred) */
+	a.v6p = a.qt && a.v6d && d->qt_live != 3 && !a.pwide &&
+		((a.t6.fmask & 3) == 2u || (a.t6.fmask & 3) == 1u);
+#ifdef XFG_DIAG
+	const char *v6e = getenv("XFG_V6P");   /* "off": every IPv6 frame deferred */
+	if (v6e && !strcmp(v6e, "off"))
+		a.v6p = 0;
+#endif
 	if (a.qt && !a.pbuf && !qt_nolog) {   /* (decided above: cannot happen) */
 		err = -EIO;
 		goto out;

@@ -1472,17 +1472,17 @@ __global__ __launch_bounds__(DF_THREADS) void xfg_defer_kernel(const xfg_kargs a
 }
 #endif
 
-template <uint32_t FEAT, bool L16, bool BOTH, bool WIDE>
+template <uint32_t FEAT, bool L16, bool BOTH, bool WIDE, bool V6P = false>
 void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
 	if (a.window <= 64 && a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
 	else if (a.window <= 64)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
 	else if (a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 	else
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH, WIDE>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 #ifdef XFG_DIAG
 	if (a.defer_sep) {
 		if (a.window <= 64)
@@ -1498,6 +1498,11 @@ void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 template <uint32_t FEAT, bool L16>
 void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
+	if constexpr ((FEAT & F_IPV6) != 0)
+		if (a.v6p) {   // (one IPv4 direction, no u32 log: the host's choice)
+			launch_pipeq2<FEAT, L16, false, false, true>(a, grid, dl, s);
+			return;
+		}
 	if (a.qt_live == 3)
 		launch_pipeq2<FEAT, L16, true, false>(a, grid, dl, s);
 	else if (a.pwide)
@@ -1648,8 +1653,8 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 		} else if (kind == 5) {
 			done = true;
 			e = window <= 64
-				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true, false, false>, QT_THREADS(64), dyn)
-				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true, false, true>, QT_THREADS(128), dyn);
+				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true, false, false, false>, QT_THREADS(64), dyn)
+				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true, false, true, false>, QT_THREADS(128), dyn);
 		}
 	}
 	if (done)

@@ -155,6 +155,9 @@ struct xfg_kargs {
 	/* quotient-index kernel with IPv6 keys live (no Ethernet key): every IPv6
 	 * frame goes to the deferred path, the IPv4 lookups through the index */
 	uint32_t v6d;
+	/* ... and (v6p) their lookups in the kernel's loop: exactly one IPv6
+	 * direction live, one IPv4 lookup direction, no u32 hit log */
+	uint32_t v6p;
 	/* Direct LDS counters: identities below dcnt (all hash maps, gbase[3],
 	 * or the IPv4 map, gbase[1]) are summed per workgroup in LDS; 0 = off */
 	uint32_t dcnt;

@@ -716,7 +716,7 @@ namespace {
 
 struct Parse4 {
 	uint32_t abort_at, l4proto, psrc, pdst, k4a, k4b;
-	bool v4ok, defer, is6;
+	bool v4ok, defer, is6, v6ok;
 };
 
 // Branch-free helpers: every operand evaluated, combined with bitwise
@@ -788,6 +788,7 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	r.k4b = __builtin_amdgcn_alignbyte(d7, d6, 2);   // saddr 26..29
 	r.v4ok = !runt & is4 & !s4 & !ihlx;
 	r.is6 = !runt & is6;
+	r.v6ok = !runt & is6 & !s6;   // an IPv6 lookup runs (before any L4 check)
 	return r;
 }
 

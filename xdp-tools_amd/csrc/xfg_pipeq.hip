@@ -67,7 +67,7 @@
 
 namespace {
 
-template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE>
+template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE, bool V6P>
 __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
 	static_assert((FEAT & F_IPV4) != 0, "IPv4-key mode needs the IPv4 feature");
@@ -88,6 +88,15 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// in R with them)
 	constexpr bool SPEC = BOTH && XFG_QT_SPEC;
 	constexpr bool R2 = BOTH && !SPEC;
+	// V6P (IPv6 keys live beside the index, one direction, kargs.v6p): the
+	// IPv6 lookups in the loop -- up to 16 IPv6 frames of a tile, their home
+	// bucket lines of the canonical IPv6 table loaded four lanes to a line
+	// (ONE load instruction), moved to the frame's lane through LDS and
+	// matched next iteration; a 17th frame, the zero key and a miss in an
+	// overflowed bucket are deferred
+	static_assert(!V6P || ((FEAT & F_IPV6) != 0 && !BOTH), "IPv6 lookups: one IPv4 direction");
+	// bucket loads per iteration issued before the windows (L, L6)
+	constexpr uint32_t NL = 2 + (SPEC ? 2 : 0) + (V6P ? 1 : 0);
 	static_assert(D == 2 || (D == 3 && LAG == 2), "window depth: 2, or 3 with a bucket lag of 2");
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	constexpr uint32_t QTAG = CT_QTAG;   // tag bit: a QT slot (hit log), not a counter identity
@@ -119,6 +128,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
 	__shared__ uint32_t s_lh[XFG_LOG_PARTS];
 	__shared__ unsigned long long s_stats[6];
+	__shared__ uint32_t s6b[V6P ? NW * 16 : 1];   // (V6P) a tile's IPv6 home buckets, by rank
+	__shared__ u32x4 s6l[V6P ? NW * 64 : 1];      // (V6P) their lines, four lanes each
 	extern __shared__ uint32_t s_dyn[];
 
 #ifdef XFG_DIAG
@@ -148,6 +159,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// (IPv6 keys live, no Ethernet key: every IPv6 frame takes the deferred
 	// path -- the whole reference walk over the canonical tables)
 	const bool v6d = (FEAT & F_IPV6) != 0 && a.v6d != 0;
+	// (V6P: the canonical IPv6 table, its one live direction)
+	const uint64_t b6base = V6P ? rfl64((uint64_t)(uintptr_t)a.t6.buckets) : 0;
+	const uint32_t nb6 = V6P ? rfl(a.t6.nbuckets) : 0u, seed6 = V6P ? rfl(a.t6.seed) : 0u;
+	const bool md6 = V6P && a.t6.max_disp != 0, k6live = V6P && a.t6.count != 0;
+	const bool d6 = (a.t6.fmask & M_DST) == M_DST;
+	const uint32_t m6 = d6 ? M_DST : M_SRC, gb6 = rfl(a.gbase[1]);
 	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
 	cn.init(a, tid, NT);
 	if (tid < 6)
@@ -332,9 +349,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		uint32_t key, b, pk, tag, key2, b2;
 		bool sel;
 		u32x4 bk0, bk1, cs0, cs1;
+		// (V6P) the IPv6 key, home bucket, rank in the tile, whether it is
+		// looked up here; this lane's quarter of a line
+		uint32_t k6[4], b6, r6;
+		bool s6;
+		u32x4 c6;
 	};
 	RSt stA = { 0, 0, pk3(A_NONE, XFG_PORT_TAB, 0), CT_NONE, 0, 0, false, { 0, 0, 0, 0 }, { 0, 0, 0, 0 },
-		    { 0, 0, 0, 0 }, { 0, 0, 0, 0 } };
+		    { 0, 0, 0, 0 }, { 0, 0, 0, 0 }, { 0, 0, 0, 0 }, 0, 0, false, { 0, 0, 0, 0 } };
 	RSt stB = stA;
 	// (both directions: the src key's entry and bucket from P; tile k-1's
 	// state after its dst lookup, for R2 next iteration; its src bucket)
@@ -369,7 +391,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// everything but the newest iteration's loads (LAG 1: tile k+1's
 		// windows; LAG 2: also the last iteration's bucket loads; depth 3:
 		// also the windows issued the iteration before)
-		constexpr uint32_t VW = CPP + 1 + (LAG - 1) * 2 + (D - 2) * (CPP + 1);
+		constexpr uint32_t VW = CPP + 1 + (LAG - 1) * NL + (D - 2) * (CPP + 1);
 		__builtin_amdgcn_s_waitcnt(0x0F70 | (VW & 15) | ((VW >> 4) << 14));
 		if constexpr (D == 3)   // (nothing that uses a load above the wait)
 			__builtin_amdgcn_sched_barrier(0);
@@ -419,9 +441,33 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			found &= rs.sel;
 			const bool defer = rs.sel & !found & ovf;
 			const uint32_t slot = rs.b * XFG_QT_SLOTS + ix;
-			const uint32_t x_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
-			const uint32_t x_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, rs.tag));
-			const uint32_t x_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
+			uint32_t x_act = pick(found, HIT, pick(defer, A_DEFER, r_act));
+			uint32_t x_tag = pick(found, QTAG | slot, pick(defer, CT_NONE, rs.tag));
+			uint32_t x_ps = pick(found | defer, XFG_PORT_TAB, r_ps);
+			if constexpr (V6P) {
+				// lookup_verdict_ipv6 (xdpfilt_prog.h:152-165): the frame's
+				// home line from its four lanes, three 16-byte keys, a flag
+				// byte each (CHECK_MAP, :56-64), the overflow bit
+				__builtin_amdgcn_wave_barrier();
+				s6l[wv * 64 + lane] = rs.c6;
+				__builtin_amdgcn_wave_barrier();
+				bool f6 = false, o6 = false;
+				uint32_t i6 = 0;
+				if (rs.s6) {
+					const u32x4 *ln = &s6l[wv * 64 + rs.r6 * 4];
+					const u32x4 q0 = ln[0], q1 = ln[1], q2 = ln[2], q3 = ln[3];
+					const bool e0 = (q0.x == rs.k6[0]) & (q0.y == rs.k6[1]) & (q0.z == rs.k6[2]) & (q0.w == rs.k6[3]);
+					const bool e1 = (q1.x == rs.k6[0]) & (q1.y == rs.k6[1]) & (q1.z == rs.k6[2]) & (q1.w == rs.k6[3]);
+					const bool e2 = (q2.x == rs.k6[0]) & (q2.y == rs.k6[1]) & (q2.z == rs.k6[2]) & (q2.w == rs.k6[3]);
+					i6 = pick(e0, 0u, pick(e1, 1u, 2u));
+					const uint32_t fl = (q3.x >> (8 * i6)) & 0xff;
+					f6 = (e0 | e1 | e2) & ((fl & m6) == m6);
+					o6 = !(e0 | e1 | e2) & ((q3.w & XFG_META_OVERFLOW) != 0) & md6;
+				}
+				x_act = pick(f6, HIT, pick(o6, A_DEFER, x_act));
+				x_tag = pick(f6, gb6 + rs.b6 * XFG_SLOTS_V6 + i6, pick(o6, CT_NONE, x_tag));
+				x_ps = pick(f6 | o6, XFG_PORT_TAB, x_ps);
+			}
 			if constexpr (SPEC) {   // the src lookup, its bucket loaded beside the dst one
 				const bool need = rs.sel & !found & !defer;
 				bool f2;
@@ -549,6 +595,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		__builtin_amdgcn_sched_barrier(0);
 		PMARK("P");
 		// ---- P: parse tile k, hash its key, plan its fallback
+		uint32_t n6 = 0;   // (V6P) the tile's IPv6 lookups, at most 16
+		rs.s6 = false;
 		if (vP && (dg & 64)) {   // (diagnostics: no parse)
 			const uint32_t gi = tP * 64 + lane;
 			rs.b = pick(gi < n, hk >> rsh, 0u);
@@ -560,7 +608,35 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const uint32_t gi = tP * 64 + lane;
 			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
-			const bool rdef = r.defer | (v6d & r.is6);
+			bool def6 = false;
+			if constexpr (V6P) {
+				// the IPv6 key (daddr at 38, saddr at 22: two bytes into a
+				// row dword), its home bucket, its rank among the tile's
+				// lookups; ranks below 16 post their bucket for L6
+				const bool k6 = valid & !r.defer & r.v6ok & k6live;
+				uint32_t w6[4];
+#pragma unroll
+				for (int i = 0; i < 4; i++)
+					w6[i] = d6 ? __builtin_amdgcn_alignbyte(myrow[10 + i], myrow[9 + i], 2)
+						   : __builtin_amdgcn_alignbyte(myrow[6 + i], myrow[5 + i], 2);
+				const bool z6 = (w6[0] | w6[1] | w6[2] | w6[3]) == 0;   // (slot nslots: deferred)
+				const unsigned long long bm6 = __ballot(k6 & !z6);
+				const uint32_t rk = lanes_below(bm6);
+				const bool sel6 = k6 & !z6 & (rk < 16);
+				def6 = k6 & !sel6;
+				const uint32_t hb6 = xfg_home(xfg_hash_v6(w6[0], w6[1], w6[2], w6[3], seed6), nb6);
+				if (sel6)
+					s6b[wv * 16 + rk] = hb6;
+				n6 = min((uint32_t)__popcll(bm6), 16u);
+#pragma unroll
+				for (int i = 0; i < 4; i++)
+					rs.k6[i] = w6[i];
+				rs.b6 = hb6;
+				rs.r6 = rk;
+				rs.s6 = sel6;
+			}
+			// (IPv6 keys live without V6P: every IPv6 frame deferred)
+			const bool rdef = r.defer | (v6d & r.is6 & !V6P) | def6;
 			const bool kok = valid & !rdef & r.v4ok & klive;
 			const uint32_t h = hk;
 			rs.b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
@@ -604,6 +680,17 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			rs.b = 0;
 			rs.pk = pk3(A_NONE, XFG_PORT_TAB, 0);
 			rs.tag = CT_NONE;
+		}
+
+		if constexpr (V6P) {
+			// ---- L6: the tile's IPv6 home lines, lane L the 16-byte quarter
+			// L & 3 of rank L >> 2's line (lanes past the tile's lookups: a
+			// line of bucket 0)
+			__builtin_amdgcn_wave_barrier();
+			const uint32_t j = (uint32_t)lane >> 2;
+			const uint32_t bb = j < n6 ? s6b[wv * 16 + j] : 0u;
+			rs.c6 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(
+				b6base + (uint64_t)bb * XFG_BUCKET_BYTES + ((uint32_t)lane & 3) * 16);
 		}
 
 		PMARK("I");
