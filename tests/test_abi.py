@@ -81,6 +81,17 @@ def host():
     f.close()
 
 
+def test_open_window_option():
+    """xfg_open_opts.window: 0 (64-byte windows), 64 or 128; anything else is
+    -EINVAL (include/xdpfilter_gpu.h)."""
+    for w in (0, 64, 128):
+        G.Filter(G.FEAT_ALL | G.FEAT_DENY, ndev=0, window=w).close()
+    for w in (32, 96, 256):
+        with pytest.raises(OSError) as e:
+            G.Filter(G.FEAT_ALL | G.FEAT_DENY, ndev=0, window=w)
+        assert e.value.errno == errno.EINVAL
+
+
 def test_host_context_basics(host):
     assert host.ndev == 0 and host.prog_name == "xdpfilt_dny_all"
     with pytest.raises(OSError) as e:

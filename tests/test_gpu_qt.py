@@ -488,3 +488,20 @@ def test_qt_index_past_one_count_pass(G):
     assert f.last_path() == 5
     assert_same(v, gpu_values(f, G, rules), f.stats(), ov, orules, ost)
     f.close()
+
+
+@pytest.mark.parametrize("stride", [128, 256, 1536])
+def test_qt_window_128_option(G, stride):
+    """xfg_open_opts.window = 128: the 128-byte-window kernels (IPv6/TCP's
+    doff at byte 66 inside the window, not deferred), with IPv6 rules of one
+    direction beside the index, on the fuzz corpus and C3/C5 traffic."""
+    rules, v4, ports = one_direction_rules(131, 20000, 2)
+    v6 = X.rand_keys(132, 3000, 16)
+    rules.v6_keys = v6
+    rules.v6_vals = np.full(len(v6), 2, np.uint64)
+    kind = 5 if stride == 1536 else 3
+    d1, l1 = X.gen_workload(133, kind, 1 << 15, stride, v4=v4, v6=v6, ports=ports)
+    d2, l2 = fuzz_at(134, 1 << 14, stride, rules, ports)
+    data = np.concatenate([d1, d2])
+    lens = np.concatenate([l1, l2])
+    run_both(G, "xdpfilt_dny_all", rules, data, lens, stride, ipv6_capacity=1 << 13, window=128)
