@@ -67,6 +67,28 @@
 
 namespace {
 
+// Deferred packets [d0, d0 + 64) of a wave's list (ndef entries): the whole
+// reference walk over the canonical tables (classify_staged), the verdict
+// stored; returns the action, the counter identity and length for the
+// caller's counting.  Whole wave.
+template <uint32_t FEAT, int W>
+__device__ __forceinline__ uint32_t qt_drain_one(const xfg_kargs &a, const uint32_t *s_ports, uint32_t *row,
+						const uint32_t *dlist, uint32_t d0, uint32_t ndef, uint32_t &tag,
+						uint32_t &len)
+{
+	const int lane = threadIdx.x & 63;
+	tag = CT_NONE;
+	len = 0;
+	const bool ok = d0 + lane < ndef;
+	const uint32_t gi = ok ? gld32(dlist + d0 + lane) : 0u;
+	if (ok)
+		len = min(load_len(a, gi), a.stride);
+	const uint32_t act = classify_staged<FEAT, W>(a, s_ports, row, ok, gi, len, tag);
+	if (ok)
+		__builtin_nontemporal_store((uint8_t)act, a.verdicts + gi);
+	return act;
+}
+
 template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE, bool V6P>
 __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
@@ -778,14 +800,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		ndef = 0;
 	}
 	for (uint32_t d0 = 0; d0 < ndef; d0 += 64) {
-		uint32_t act = A_NONE, tag = CT_NONE, len = 0;
-		const bool ok = d0 + lane < ndef;
-		const uint32_t gi = ok ? gld32(dlist + d0 + lane) : 0u;
-		if (ok)
-			len = min(load_len(a, gi), a.stride);
-		act = classify_staged<FEAT, W>(a, s_ports, const_cast<uint32_t *>(myrow), ok, gi, len, tag);
-		if (ok)
-			__builtin_nontemporal_store((uint8_t)act, a.verdicts + gi);
+		uint32_t tag, len;
+		const uint32_t act = qt_drain_one<FEAT, W>(a, s_ports, const_cast<uint32_t *>(myrow), dlist, d0, ndef,
+							   tag, len);
 		count(tag, XFG_PORT_TAB);
 		stat(act, len);
 	}
