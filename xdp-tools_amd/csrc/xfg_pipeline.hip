@@ -727,14 +727,16 @@ __device__ __forceinline__ uint32_t pick(bool c, uint32_t x, uint32_t y)
 	return y ^ ((x ^ y) & (0u - (uint32_t)c));
 }
 
+// (the window's dwords 3..16 as values: dw[j] = dword j of the frame; the
+// row form below reads them from an LDS row one at a time)
 template <uint32_t FEAT, int W>
-__device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
+__device__ __forceinline__ Parse4 parse_bf_dw(const uint32_t (&dw)[17], uint32_t len)
 {
-	const uint32_t d3 = row[3], d5 = row[5], d6 = row[6], d7 = row[7], d8 = row[8], d9 = row[9];
-	const uint32_t d11 = row[11], d13 = row[13], d14 = row[14];
+	const uint32_t d3 = dw[3], d5 = dw[5], d6 = dw[6], d7 = dw[7], d8 = dw[8], d9 = dw[9];
+	const uint32_t d11 = dw[11], d13 = dw[13], d14 = dw[14];
 	uint32_t d16 = 0;
 	if constexpr (W >= 68)
-		d16 = row[16];
+		d16 = dw[16];
 	const uint32_t et = d3 & 0xffff;   // raw (network-order) ethertype
 	const bool runt = len < 14;        // parse_ethhdr
 	const bool is4 = et == 0x0008, is6 = et == 0xdd86;
@@ -749,7 +751,7 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	constexpr bool ARPP = (FEAT & F_IPV4) != 0;
 	bool arpbad = false;
 	if constexpr (ARPP)
-		arpbad = arp & ((len < 42) | ((d3 >> 16) != 0x0100u) | (row[4] != 0x04060008u));
+		arpbad = arp & ((len < 42) | ((d3 >> 16) != 0x0100u) | (dw[4] != 0x04060008u));
 	// IPv4 (__parse_iphdr, frags ok, no version check): ihl 5 keeps L4 at 34
 	const bool s4 = len < 34;
 	const uint32_t ihl = (d3 >> 16) & 0xf;
@@ -790,6 +792,23 @@ __device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
 	r.is6 = !runt & is6;
 	r.v6ok = !runt & is6 & !s6;   // an IPv6 lookup runs (before any L4 check)
 	return r;
+}
+
+template <uint32_t FEAT, int W>
+__device__ __forceinline__ Parse4 parse_bf(const uint32_t *row, uint32_t len)
+{
+	uint32_t dw[17] = {};
+	dw[3] = row[3];
+	dw[4] = ((FEAT & F_IPV4) != 0) ? row[4] : 0u;
+#pragma unroll
+	for (int j = 5; j <= 9; j++)
+		dw[j] = row[j];
+	dw[11] = row[11];
+	dw[13] = row[13];
+	dw[14] = row[14];
+	if constexpr (W >= 68)
+		dw[16] = row[16];
+	return parse_bf_dw<FEAT, W>(dw, len);
 }
 
 // The port rule of `key` in the workgroup's LDS copy: its flags, and with

@@ -49,6 +49,12 @@
 #ifndef XFG_QT_SPEC      /* both directions: src buckets loaded with the dst ones (A/B) */
 #define XFG_QT_SPEC 0
 #endif
+#ifndef XFG_QT_OWNC      /* a wave owns PPW consecutive log partitions (0: every NW-th) */
+#define XFG_QT_OWNC 1
+#endif
+#ifndef XFG_QT_ROWQ      /* rows of 16-byte-aligned stride: b128 LDS writes and reads (0: b32) */
+#define XFG_QT_ROWQ 1
+#endif
 #ifndef XFG_QT_NTLEN     /* lengths loaded non-temporal (A/B) */
 #define XFG_QT_NTLEN 0
 #endif
@@ -96,7 +102,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr int NW = QT_WAVES(W);
 	constexpr int NT = 64 * NW;
 	constexpr int CPP = W / 16;
-	constexpr int ROWDW = W / 4 + 1;
+	// (ROWQ: a 16-byte-aligned row stride of 20 / 36 dwords -- b128 accesses
+	// of 16 lanes at a time fall in disjoint banks -- written and read a
+	// quarter-line at a time, the parse working from registers)
+	constexpr bool ROWQ = XFG_QT_ROWQ != 0;
+	constexpr int ROWDW = ROWQ ? W / 4 + 4 : W / 4 + 1;
+	constexpr int NQ = W >= 68 ? 5 : 4;   // (ROWQ) the row's first 16-byte pieces the parse reads
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t LAG = XFG_QT_LAG;
@@ -125,14 +136,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// Write-combined hit log.  A QT hit of partition p = log_part(slot)
 	// goes, as its 16-bit local index, into p's ring of WR entries in LDS
 	// (reserve a place: s_res[p]; take a ticket: s_hd[2p]; write; count the
-	// write done: s_hd[2p + 1]).  Wave p % NW owns p: once an iteration it
+	// write done: s_hd[2p + 1]).  Wave p / PPW owns p: once an iteration it
 	// moves completed chunks of WF entries (all tickets written: done ==
 	// head) into the workgroup's slice of p's partition buffer -- the
 	// layout log_partition writes and xfg_log_count_kernel reads -- and
 	// gives their places back.  A hit that finds the ring full (a hot key)
 	// is summed in the LDS counter cache instead (QT tag), as is a chunk
 	// that would overrun the slice.  No per-wave log, no workgroup-end sort.
-	constexpr uint32_t PPW = XFG_LOG_PARTS / NW;   // partitions a wave owns: lane * NW + wave
+	constexpr uint32_t PPW = XFG_LOG_PARTS / NW;   // partitions a wave owns (ownp)
 	static_assert(PPW * NW == XFG_LOG_PARTS && PPW <= 64, "partition ownership");
 	// (WIDE: an index past 2^20 buckets -- local indices past 16 bits -- logs
 	// u32 entries, a ring of the same bytes: half the entries; with 64-byte
@@ -141,7 +152,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr uint32_t WR = (W <= 64 ? XFG_QT_WC_R : XFG_QT_WC_R128) / (WIDE ? 2 : 1);
 	constexpr uint32_t WF = W <= 64 ? XFG_QT_WC_F / (WIDE ? 2 : 1) : WR / 2;   // flush chunk
 	static_assert((WR & (WR - 1)) == 0 && WF <= 64, "ring: a power of two");
-	__shared__ uint32_t win[NW * 64 * ROWDW];
+	__shared__ __attribute__((aligned(16))) uint32_t win[NW * 64 * ROWDW];
 	__shared__ ring_t s_ring[XFG_LOG_PARTS * WR];
 	__shared__ uint32_t s_res[XFG_LOG_PARTS];
 	__shared__ __attribute__((aligned(8))) uint32_t s_hd[2 * XFG_LOG_PARTS];
@@ -205,7 +216,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		s_hd[2 * i + 1] = 0;
 	}
 	// this lane's partition (lanes below PPW), the entries it has moved out
-	const uint32_t wc_p = (uint32_t)lane * NW + (uint32_t)wv;
+	// (OWNC: wave wv owns partitions wv * PPW .. + PPW - 1, so its lanes' head /
+	// done words are consecutive: one conflict-free 8-byte LDS read)
+	auto ownp = [&](uint32_t j) { return XFG_QT_OWNC ? (uint32_t)wv * PPW + j : j * NW + (uint32_t)wv; };
+	const uint32_t wc_p = ownp((uint32_t)lane);
 	uint32_t wc_fl = 0;
 	const uint64_t wc_slice0 = (uint64_t)blockIdx.x * a.pcap;
 	const uint64_t wc_pstep = (uint64_t)a.pslices * a.pcap;
@@ -258,7 +272,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// move entries [fl, fl + cnt) of lane j's partition to its slice (cnt
 	// <= WR; positions past pcap: the counter cache instead)
 	auto wc_move = [&](uint32_t j, uint32_t fl, uint32_t cnt) {
-		const uint32_t p = j * NW + (uint32_t)wv;
+		const uint32_t p = ownp(j);
 		for (uint32_t o = lane; o < cnt; o += 64) {
 			const uint32_t e = s_ring[p * WR + ((fl + o) & (WR - 1))];
 			const uint32_t pos = fl + o;
@@ -294,7 +308,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const uint32_t fl = __builtin_amdgcn_readlane(wc_fl, j);
 			wc_move(j, fl, WF);
 			if (lane == 0)   // (after the ring reads: LDS keeps a wave's order)
-				atomicSub(&s_res[j * NW + wv], WF);
+				atomicSub(&s_res[ownp(j)], WF);
 			wc_fl += (uint32_t)lane == j ? WF : 0u;
 		}
 	};
@@ -567,10 +581,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 					const int c = it * 64 + lane;
 					const int pk = c / CPP, sub = c % CPP;
 					uint32_t *dst = &rows[pk * ROWDW + sub * 4];
-					dst[0] = cur[it].x;
-					dst[1] = cur[it].y;
-					dst[2] = cur[it].z;
-					dst[3] = cur[it].w;
+					if constexpr (ROWQ) {
+						*reinterpret_cast<u32x4 *>(dst) = cur[it];
+					} else {
+						dst[0] = cur[it].x;
+						dst[1] = cur[it].y;
+						dst[2] = cur[it].z;
+						dst[3] = cur[it].w;
+					}
 				}
 			} else {   // (diagnostics: the data kept live, not staged)
 #pragma unroll
@@ -591,8 +609,25 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// loads (a fixed count); one whose frame is not IPv4 loads bucket 0
 		// (a shared line).
 		uint32_t hk = 0, lbk = 0, hk2 = 0, lbk2 = 0;
+		uint32_t dw[17] = {};   // (ROWQ) the row's dwords, read four at a time
+		if constexpr (ROWQ) {
+			if (vP) {
+#pragma unroll
+				for (int q = 0; q < NQ; q++) {
+					const u32x4 v = reinterpret_cast<const u32x4 *>(myrow)[q];
+					dw[4 * q] = v.x;
+					if (4 * q + 1 < 17)
+						dw[4 * q + 1] = v.y;
+					if (4 * q + 2 < 17)
+						dw[4 * q + 2] = v.z;
+					if (4 * q + 3 < 17)
+						dw[4 * q + 3] = v.w;
+				}
+			}
+		}
+		auto rowd = [&](int j) { return ROWQ ? dw[j] : myrow[j]; };
 		if (vP) {
-			const uint32_t e3 = myrow[3], e6 = myrow[6], e7 = myrow[7], e8 = myrow[8];
+			const uint32_t e3 = rowd(3), e6 = rowd(6), e7 = rowd(7), e8 = rowd(8);
 			const uint32_t key = dlive ? __builtin_amdgcn_alignbyte(e8, e7, 2) : __builtin_amdgcn_alignbyte(e7, e6, 2);
 			hk = xfg_qt_hash(key, qseed);
 			const bool ip4 = (e3 & 0xffffu) == 0x0008u;
@@ -628,7 +663,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			rs.tag = CT_NONE;
 		} else if (vP) {
 			const uint32_t gi = tP * 64 + lane;
-			const Parse4 r = parse_bf<FEAT, W>(myrow, len);
+			Parse4 r;
+			if constexpr (ROWQ)
+				r = parse_bf_dw<FEAT, W>(dw, len);
+			else
+				r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
 			bool def6 = false;
 			if constexpr (V6P) {
@@ -639,8 +678,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				uint32_t w6[4];
 #pragma unroll
 				for (int i = 0; i < 4; i++)
-					w6[i] = d6 ? __builtin_amdgcn_alignbyte(myrow[10 + i], myrow[9 + i], 2)
-						   : __builtin_amdgcn_alignbyte(myrow[6 + i], myrow[5 + i], 2);
+					w6[i] = d6 ? __builtin_amdgcn_alignbyte(rowd(10 + i), rowd(9 + i), 2)
+						   : __builtin_amdgcn_alignbyte(rowd(6 + i), rowd(5 + i), 2);
 				const bool z6 = (w6[0] | w6[1] | w6[2] | w6[3]) == 0;   // (slot nslots: deferred)
 				const unsigned long long bm6 = __ballot(k6 & !z6);
 				const uint32_t rk = lanes_below(bm6);
