@@ -84,8 +84,9 @@ struct xfg_open_opts {
 	uint32_t eth_capacity;
 	uint32_t hash_seed;      /* 0 => fixed default seed */
 	/* IPv4 maps with at least this many keys are looked up through the
-	 * one-read quotient index when it applies (fixed-stride batches, one
-	 * live IPv4 lookup direction, the same flags on every device): 0 =>
+	 * one-read quotient index when it applies (fixed-stride batches, no
+	 * live Ethernet key, one or both IPv4 lookup directions live, the same
+	 * flags on every device): 0 =>
 	 * default (2^18), UINT32_MAX => never.  Results never depend on it. */
 	uint32_t qt_min_keys;
 	/* Header window of the pipelined kernels for fixed-stride batches

@@ -9,7 +9,7 @@ per-action stats.  Contract: xdp-filter/xdpfilt_prog.h:56-64,214-310.
   C2  xdpfilt_dny_ip, 1,000 IPv4 dst rules, ipv4_capacity=1000 (the direct
       LDS counter path, kargs.dcnt), 64 B dense frames, 2^22 packets
   C3  xdpfilt_dny_all, 1M IPv4 dst rules at capacity 1M + 16 dst-port rules,
-      64 B frames, 2^22 packets (the IPv4-key pipelined kernel, hit log)
+      64 B frames, 2^22 packets (the quotient-index kernel, hit log)
   C4  xdpfilt_dny_all, IMIX 64/570/1514 at a 1536 B stride, 1M IPv4 rules
   C5  xdpfilt_dny_all, 15M IPv4 + 1M IPv6 dst rules + 1024 dst-port rules,
       1514 B frames at a 1536 B stride, 2^18 packets, device-resident (the
@@ -111,7 +111,7 @@ def test_c5_16m_rules_1514b_device_and_host(G):
     rules, v4, v6, ports = config_rules(5, 15_000_000, 1_000_000, 1024)
     data, lens = X.gen_workload(5, 5, 1 << 18, 1536, v4=v4, v6=v6, ports=ports)
     # (the quotient index of 2^21 buckets -- more slots than packets here, so
-    # its hits count through the LDS cache and atomics, no hit log -- and
-    # the IPv6 frames through the deferred-packet kernel)
+    # its hits count through the LDS cache and atomics, no hit log -- with
+    # the IPv6 lookups in its loop, V6P: one line read per IPv6 frame)
     check(G, "xdpfilt_dny_all", rules, data, lens, 1536, host=True, path=5,
           ipv4_capacity=15_000_000, ipv6_capacity=1_000_000)

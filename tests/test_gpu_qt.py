@@ -384,6 +384,83 @@ def test_qt_single_edits_between_batches(G):
     f.close()
 
 
+def test_qt_single_edits_concurrent_with_classify(G):
+    """single inserts on one thread while another thread
+    launches classifies.  Each insert is the 17th key homed in an exactly full
+    index bucket, so entry 15 becomes the overflow marker and the key that
+    was there -- still live, still hit by the traffic -- moves to the
+    canonical table.  Hits a classify counted through the old bucket must be
+    folded before the bucket and its trans[] entries are replaced (qt_edit
+    folds in the same device-lock section), so every live key's count equals
+    the packets that hit it: M identical batches = M x one pass of the
+    restatement.  Contract: per-CPU counters edited between packets,
+    xdp-filter/xdp-filter.c:93-157; CHECK_MAP, xdpfilt_prog.h:56-64."""
+    import threading
+    feat = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    base, v4, ports = one_direction_rules(171, 20000, 2)
+    busy = set(qt_bucket(base.v4_keys).tolist())
+    rng = np.random.default_rng(172)
+    cand = np.unique(rng.integers(0, 2**32, 1 << 22, dtype=np.uint64).astype(np.uint32))
+    cu8 = cand.view(np.uint8).reshape(-1, 4)
+    b = qt_bucket(cu8)
+    order = np.argsort(b, kind="stable")
+    b, cu8 = b[order], cu8[order]
+    starts = np.searchsorted(b, np.arange(1 << QT_BITS))
+    counts = np.bincount(b, minlength=1 << QT_BITS)
+    pick_b = [bb for bb in np.nonzero(counts >= 17)[0] if bb not in busy][:256]
+    full = np.concatenate([cu8[starts[bb]:starts[bb] + 16] for bb in pick_b])   # 16 per bucket
+    extra = np.stack([cu8[starts[bb] + 16] for bb in pick_b])                  # each one's 17th
+    rules = X.RuleSet()
+    rules.v4_keys = np.concatenate([full, base.v4_keys])
+    rules.v4_vals = np.concatenate([np.full(len(full), 2, np.uint64), base.v4_vals])
+    rules.ports = base.ports
+    data, lens = X.gen_workload(173, 3, 1 << 16, 64, v4=rules.v4_keys, ports=ports)
+    d = data.reshape(-1, 64)
+    ip4 = np.nonzero((d[:, 12] == 8) & (d[:, 13] == 0) & (lens >= 62))[0][:40000]
+    d[ip4, 30:34] = full[np.arange(len(ip4)) % len(full)]
+    ov, orules, ost = X.run_oracle(feat, data, lens, rules, stride=64, nthreads=8)
+
+    f = make_filter(G, "xdpfilt_dny_all", qt_min_keys=1, ipv4_capacity=1 << 16)
+    f.load_rules(rules)
+    d_data, d_lens, d_v = f.alloc(data.nbytes), f.alloc(lens.nbytes), f.alloc(len(lens))
+    d_data.upload(data)
+    d_lens.upload(lens)
+    M = 48
+    errs = []
+
+    def classify_loop():
+        try:
+            for _ in range(M):
+                f.classify(d_data.ptr, d_lens.ptr, len(lens), 64, d_v.ptr)
+        except Exception as e:  # reported below
+            errs.append(e)
+
+    th = threading.Thread(target=classify_loop)
+    th.start()
+    for k in extra:
+        f.update(G.MAP_IPV4, bytes(k), 2)
+    th.join()
+    f.sync()
+    assert not errs, errs
+    assert f.last_path() == 5
+    v = np.zeros(len(lens), np.uint8)
+    d_v.download(v)
+    np.testing.assert_array_equal(v, ov)
+    # live keys: M passes' hits on top of their loaded values; the inserted keys: untouched
+    one = (orules.v4_vals >> np.uint64(6)) - (rules.prepared().v4_vals >> np.uint64(6))
+    exp = X.RuleSet()
+    exp.v4_keys = np.concatenate([rules.prepared().v4_keys, extra])
+    pv = rules.prepared().v4_vals
+    exp.v4_vals = np.concatenate([pv + ((one * np.uint64(M)) << np.uint64(6)),
+                                  np.full(len(extra), 2, np.uint64)])
+    got = f.values_of(G.MAP_IPV4, exp.v4_keys)
+    np.testing.assert_array_equal(got, exp.v4_vals)
+    np.testing.assert_array_equal(f.stats(), ost * np.uint64(M))
+    for x in (d_data, d_lens, d_v):
+        x.free()
+    f.close()
+
+
 def test_qt_falls_back_when_the_log_cannot_run(G):
     """qt_min_keys=1 with maps small enough that every counter has a direct
     LDS counter: the index is not used -- the IPv4-key kernel's direct LDS

@@ -13,7 +13,7 @@ P=xdp-tools_amd
 S=${SRC:-$P/csrc}
 T=$(mktemp -d)
 for c in xfg_ctx xfg_table xfg_io; do
-  cc -O2 -g -fPIC -Wall -Wno-unused-parameter -std=gnu11 -DXFG_DIAG -Iinclude -I$S -I/opt/rocm/include \
+  cc $(printf "%s\n" "$@" | grep -E "^-DXFG_QT_MIN_BITS" || true) -O2 -g -fPIC -Wall -Wno-unused-parameter -std=gnu11 -DXFG_DIAG -Iinclude -I$S -I/opt/rocm/include \
     -D__HIP_PLATFORM_AMD__ -c $S/$c.c -o $T/$c.o
 done
 /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wall -DXFG_DIAG "$@" \

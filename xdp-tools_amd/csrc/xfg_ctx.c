@@ -119,6 +119,13 @@ struct xfg_dev {
 	uint32_t *tlog, *pfill;         /* hit log: wave regions, slice fills */
 	uint16_t *pbuf;                 /* hit log: partition slices */
 	uint64_t tlog_bytes, pbuf_bytes, pfill_bytes;
+	/* quotient-index logs not yet counted: log_pend launches of log_grid
+	 * workgroups, side by side in the partition buffers, counted by one
+	 * count kernel with log_args (their shape) -- when the buffers are
+	 * full, before any read of the counts (qt_fold_locked) and before a
+	 * launch of another shape */
+	uint32_t log_pend, log_grid;
+	struct xfg_kargs log_args;
 	uint32_t *rec;                  /* split classify: parse-pass records */
 	uint64_t rec_bytes;
 	unsigned long long *cstatus;    /* verdict compaction: tile status words */
@@ -166,6 +173,7 @@ struct xfg_ctx {
 /* Default smallest IPv4 map that takes the quotient index (its 2^17 buckets
  * are 4 MiB: below this the canonical table and its prefilter stay in L2). */
 #define XFG_QT_MIN_KEYS (1u << 18)
+#define XFG_LOG_PEND_MAX 4u   /* quotient-index launches per count kernel */
 
 /* ------------------------------------------------------------------ misc */
 static const struct { const char *name; uint32_t feat; } prog_table[] = {
@@ -614,14 +622,31 @@ static unsigned long long *hits_view(xfg_ctx *ctx, struct xfg_dev *d, int mi)
 	return ctx->reduced ? d->m[mi].red_hits : d->m[mi].hits;
 }
 
+/* Count the pending quotient-index logs into the QT-order counts (d->lock
+ * held): one count kernel over every pending launch's slices. */
+static int log_flush_locked(struct xfg_dev *d)
+{
+	if (!d->log_pend)
+		return 0;
+	struct xfg_kargs c = d->log_args;
+	c.pcount = d->log_pend * d->log_grid;
+	d->log_pend = 0;
+	int err = hip_err(hipSetDevice(d->ordinal));
+	if (!err)
+		err = xfg_launch_log_count(&c, d->stream);
+	return err;
+}
+
 /* Add @d's QT-order hit counts into its canonical IPv4 counters, through the
  * index's current qt_trans (d->lock held): in stream order after every
- * classify that counted into them. */
+ * classify that counted into them (and after the count kernel of every
+ * log still pending). */
 static int qt_fold_locked(struct xfg_dev *d)
 {
-	if (!d->qt_pending)
-		return 0;
-	int err = hip_err(hipSetDevice(d->ordinal));
+	int err = log_flush_locked(d);
+	if (err || !d->qt_pending)
+		return err;
+	err = hip_err(hipSetDevice(d->ordinal));
 	if (!err)
 		err = xfg_launch_qt_fold(d->qt_hits, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
 	if (!err)
@@ -758,8 +783,14 @@ static int qt_edit(xfg_ctx *ctx, uint64_t slot, const void *key, uint8_t old, ui
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
 		pthread_mutex_lock(&d->lock);
-		if (d->qt_gen == ctx->qt_gen) {
-			int e = 0;
+		/* (a classify launched since slot_store's fold counted through the
+		 * old bucket: fold it in the same lock section as the bucket write,
+		 * as qt_refresh does, so no count is read through the new trans[]) */
+		int e = qt_fold_locked(d);
+		if (e) {
+			if (!err)
+				err = e;
+		} else if (d->qt_gen == ctx->qt_gen) {
 			for (uint32_t im = 0; im < q->nimg && !e; im++) {
 				if (!chg[im])
 					continue;
@@ -776,6 +807,8 @@ static int qt_edit(xfg_ctx *ctx, uint64_t slot, const void *key, uint8_t old, ui
 		pthread_mutex_unlock(&d->lock);
 	}
 	ctx->qt_gen = gen;
+	if (err)   /* (a device whose copy may not match the map: rebuild before the next use) */
+		ctx->qt_dirty = 1;
 	return err;
 }
 
@@ -795,8 +828,11 @@ static int slot_store(xfg_ctx *ctx, int mi, uint64_t slot, const uint64_t *vals,
 	int e0 = qt_fold(ctx, mi);
 	if (!e0 && mi == 0 && old != ctx->flag_or[0][slot])
 		e0 = qt_edit(ctx, slot, key, old, ctx->flag_or[0][slot]);
-	if (e0)
+	if (e0) {
+		if (mi == 0)   /* (flags_note skipped the rebuild mark for the patch that failed) */
+			ctx->qt_dirty = 1;
 		return e0;
+	}
 	for (int i = 0; i < ctx->ndev; i++) {
 		struct xfg_dev *d = &ctx->dev[i];
 		uint8_t f = vals[i] & 63;
@@ -1435,9 +1471,9 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 		a->port_count = 0;
 	}
 #endif
-	/* the quotient index (kind 5 kernel): the IPv4-key kernel with exactly
-	 * one live IPv4 lookup direction, the same flags on every device, and a
-	 * map large enough that the prefilter + bucket-line chain leaves L2;
+	/* the quotient index (kind 5 kernel): the IPv4-key kernel with one or
+	 * both IPv4 lookup directions live, the same flags on every device, and
+	 * a map large enough that the prefilter + bucket-line chain leaves L2;
 	 * its hit log must fit the count kernel's histogram */
 	if (a->pipe && (a->km || km6) && !a->split) {
 		/* (both directions live: up to two images, twice the QT slots) */
@@ -1641,34 +1677,62 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	/* (a range past one histogram: the count kernel takes it in passes; past
 	 * 65536 local indices the slices hold u32) */
 	const int pwide = hist > 65536;
-	if (!log_off && !qt_nolog && hist <= (uint64_t)XFG_LOG_HIST_MAX * XFG_LOG_PASSES_MAX &&
-	    grid <= XFG_LOG_SLICES_MAX) {
-		/* slice (partition, workgroup): twice a uniform share of the
-		 * most the workgroup's waves can log (a fuller one spills) */
-		uint64_t wg_max = (per_wg / 64) * (uint64_t)a.defer_cap;
-		uint64_t pcap = (2 * ((wg_max + XFG_LOG_PARTS - 1) / XFG_LOG_PARTS) + 64 + 7) & ~7ull;
+	const int logs = !log_off && !qt_nolog && hist <= (uint64_t)XFG_LOG_HIST_MAX * XFG_LOG_PASSES_MAX &&
+			 grid <= XFG_LOG_SLICES_MAX;
+	/* slice (partition, workgroup): twice a uniform share of the most the
+	 * workgroup's waves can log (a fuller one spills) */
+	const uint64_t wg_max = (per_wg / 64) * (uint64_t)a.defer_cap;
+	const uint64_t pcap = (2 * ((wg_max + XFG_LOG_PARTS - 1) / XFG_LOG_PARTS) + 64 + 7) & ~7ull;
+	/* the quotient-index kernel's logs of up to K launches side by side in
+	 * the partition buffers, counted by one count kernel (its fixed cost
+	 * -- a pass over every QT-order count -- paid once per K launches);
+	 * every other log is counted after its own launch */
+	uint64_t K = 1;
+	if (logs && a.qt) {
+		K = XFG_LOG_PEND_MAX;
+#ifdef XFG_DIAG
+		const char *lp = getenv("XFG_LOG_PEND");   /* launches per count kernel (1: round 4) */
+		if (lp && *lp)
+			K = strtoul(lp, NULL, 0) ? strtoul(lp, NULL, 0) : 1;
+#endif
+		while (K > 1 && K * grid > XFG_LOG_SLICES_MAX)
+			K--;
+	}
+	/* logs pending from earlier launches: counted first unless this one
+	 * appends to them (the same shape, the same counts) */
+	const int append = logs && K > 1 && d->log_pend && d->log_grid == grid &&
+			   d->log_args.pcap == pcap && d->log_args.pslices == K * grid &&
+			   d->log_args.log_span == hist && d->log_args.pwide == (uint32_t)pwide &&
+			   d->log_args.qt_hits == a.qt_hits && d->log_args.qt_n == a.qt_n;
+	if (d->log_pend && !append && (err = log_flush_locked(d)))
+		goto out;
+	if (logs) {
 		/* (the quotient-index kernel combines its log in LDS and writes
 		 * the partition buffers itself: no per-wave regions) */
 		if ((!a.qt && (err = scratch(d, (void **)&d->tlog, &d->tlog_bytes,
 					     grid * (per_wg / 64) * (uint64_t)a.defer_cap * 4))) ||
 		    (err = scratch(d, (void **)&d->pbuf, &d->pbuf_bytes,
-				   ((uint64_t)XFG_LOG_PARTS * grid * pcap + 1024) * (pwide ? 4 : 2))) ||   /* (+ the count kernel's overread) */
+				   ((uint64_t)XFG_LOG_PARTS * K * grid * pcap + 1024) * (pwide ? 4 : 2))) ||   /* (+ the count kernel's overread) */
 		    (err = scratch(d, (void **)&d->pfill, &d->pfill_bytes,
-				   (uint64_t)XFG_LOG_PARTS * grid * 4)))
+				   (uint64_t)XFG_LOG_PARTS * K * grid * 4)))
 			goto out;
 		a.tlog = a.qt ? NULL : d->tlog;
 		a.pbuf = d->pbuf;
 		a.pfill = d->pfill;
 		a.pcap = (uint32_t)pcap;
-		a.pslices = (uint32_t)grid;
+		a.pslices = (uint32_t)(K * grid);
+		a.pslice0 = 0;
+		a.pcount = (uint32_t)grid;
 		a.log_hist = (uint32_t)(hist < XFG_LOG_HIST_MAX ? hist : XFG_LOG_HIST_MAX);
 		a.log_span = (uint32_t)hist;
 		a.pwide = (uint32_t)pwide;
 	}
-	/* IPv6 rules beside the index: their lookups in the kernel's loop when
-	 * exactly one IPv6 direction can hit (else every IPv6 frame deferred) */
-	a.v6p = a.qt && a.v6d && d->qt_live != 3 && !a.pwide &&
-		((a.t6.fmask & 3) == 2u || (a.t6.fmask & 3) == 1u);
+	/* IPv6 rules beside the index: their lookups in the kernel's loop (1:
+	 * one IPv6 direction can hit, one line a frame; 2: both, the src line
+	 * beside the dst one), with one IPv4 direction live -- with both, every
+	 * IPv6 frame is deferred */
+	a.v6p = !(a.qt && a.v6d && d->qt_live != 3) ? 0u
+		: (a.t6.fmask & 3) == 3u ? 2u : (a.t6.fmask & 3) != 0 ? 1u : 0u;
 #ifdef XFG_DIAG
 	const char *v6e = getenv("XFG_V6P");   /* "off": every IPv6 frame deferred */
 	if (v6e && !strcmp(v6e, "off"))
@@ -1690,9 +1754,17 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * shares the CUs and slowed the classify more than it hid:
 	 * profiles/r04_s11_count_overlap.log) */
 	for (int i = 0; i < iters && !err; i++) {
+		if (a.pbuf && K > 1)
+			a.pslice0 = d->log_pend * (uint32_t)grid;
 		err = xfg_launch_classify(ctx->prog_features, &a, (unsigned)grid, d->stream);
-		if (!err)
+		if (!err && a.pbuf && K > 1) {
+			d->log_args = a;
+			d->log_grid = (uint32_t)grid;
+			if (++d->log_pend == K)
+				err = log_flush_locked(d);
+		} else if (!err) {
 			err = xfg_launch_log_count(&a, d->stream);
+		}
 	}
 	if (!err)
 		d->last_kind = kind;
@@ -1797,6 +1869,13 @@ int xfg_classify_timed(xfg_ctx *ctx, int dev, const struct xfg_batch *b, uint8_t
 	HIPCHK(hipSetDevice(d->ordinal));
 	HIPCHK(hipEventRecord(d->ev0, d->stream));
 	if ((err = launch_batch(ctx, d, &a, NULL, iters)))
+		goto fail;
+	/* (the logs still pending are counted inside the timed region: the
+	 * iterations' work is complete when ev1 fires) */
+	pthread_mutex_lock(&d->lock);
+	err = log_flush_locked(d);
+	pthread_mutex_unlock(&d->lock);
+	if (err)
 		goto fail;
 	HIPCHK(hipEventRecord(d->ev1, d->stream));
 	HIPCHK(hipEventSynchronize(d->ev1));

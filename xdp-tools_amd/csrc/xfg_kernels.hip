@@ -942,7 +942,7 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 	const uint64_t r0 = (uint64_t)blockIdx.x * NW * a.defer_cap;
 	// this workgroup's slice of every partition: position 0, its count
 	// stored for the count kernel (entries past pcap spill to atomics)
-	const uint64_t slice0 = (uint64_t)blockIdx.x * a.pcap;
+	const uint64_t slice0 = (uint64_t)(blockIdx.x + a.pslice0) * a.pcap;
 	const uint64_t pstep = (uint64_t)a.pslices * a.pcap;
 	for (int i = tid; i < (int)XFG_LOG_PARTS; i += nthr) {
 		s_h[i] = 0;
@@ -958,7 +958,7 @@ __device__ __forceinline__ void log_partition(const xfg_kargs &a, const uint32_t
 	}
 	__syncthreads();
 	for (int p = tid; p < (int)XFG_LOG_PARTS; p += nthr) {
-		gst32(a.pfill + (uint64_t)p * a.pslices + blockIdx.x, s_hist ? s_hist[p] : s_h[p]);
+		gst32(a.pfill + (uint64_t)p * a.pslices + a.pslice0 + blockIdx.x, s_hist ? s_hist[p] : s_h[p]);
 		s_h[p] = 0;
 	}
 	__syncthreads();
@@ -1282,7 +1282,8 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	const uint32_t tid = threadIdx.x, p = blockIdx.x % XFG_LOG_PARTS, lane = tid & 63, w = tid >> 6;
 	const uint32_t j0 = (blockIdx.x / XFG_LOG_PARTS) * hist_n;
 	constexpr uint32_t NWV = LC_THREADS / 64, U = 8, J = XFG_LOG_HIST_MAX / LC_THREADS;
-	const uint32_t S = a.pslices, cap = a.pcap;
+	// (S slices to read; PS between partitions: pending launches' logs side by side)
+	const uint32_t S = a.pcount, PS = a.pslices, cap = a.pcap;
 	// the identity span: hash-map + port counters, or the QT slots
 	const uint32_t total = a.qt ? a.qt_n : a.gbase[3] + 65536u;
 	// counters of histogram entries tid + j * LC_THREADS: identity, value
@@ -1297,7 +1298,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 		gid[j] = k < hist_n && l < a.log_span && g < total ? (a.qt_hits ? g : a.qt ? a.qt_trans[g] : g)
 								   : CT_NONE;
 	}
-	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * S + tid] : 0u;
+	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * PS + tid] : 0u;
 	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
 		hist[i] = 0;
 #ifdef XFG_DIAG
@@ -1312,7 +1313,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 		s_fill[tid] = min(fl, cap);
 	__syncthreads();
 	if (a.pwide) {   // (u32 local indices, a range beyond one pass)
-		const uint32_t *wb = reinterpret_cast<const uint32_t *>(a.pbuf) + (uint64_t)p * S * cap;
+		const uint32_t *wb = reinterpret_cast<const uint32_t *>(a.pbuf) + (uint64_t)p * PS * cap;
 		for (uint32_t sl = w; sl < S; sl += NWV) {
 			const uint32_t np = s_fill[sl];
 			for (uint32_t i = lane; i < np; i += 64) {
@@ -1322,7 +1323,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 			}
 		}
 	}
-	const uint16_t *base = a.pbuf + (uint64_t)p * S * cap;
+	const uint16_t *base = a.pbuf + (uint64_t)p * PS * cap;
 	// (a wave load covers 512 entries of a slice -- 16 bytes a lane: about a
 	// uniform slice at the bench's batch; pcap is a multiple of 8, so every
 	// slice starts 16-byte aligned; the buffer has 512 entries of slack)
@@ -1472,17 +1473,17 @@ __global__ __launch_bounds__(DF_THREADS) void xfg_defer_kernel(const xfg_kargs a
 }
 #endif
 
-template <uint32_t FEAT, bool L16, bool BOTH, bool WIDE, bool V6P = false>
+template <uint32_t FEAT, bool L16, bool BOTH, bool WIDE, uint32_t V6 = 0>
 void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
 	if (a.window <= 64 && a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH, WIDE, V6>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
 	else if (a.window <= 64)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH, WIDE, V6>), dim3(grid), dim3(QT_THREADS(64)), dl, s, a);
 	else if (a.dense)
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, true, L16, BOTH, WIDE, V6>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 	else
-		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH, WIDE, V6P>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 128, false, L16, BOTH, WIDE, V6>), dim3(grid), dim3(QT_THREADS(128)), dl, s, a);
 #ifdef XFG_DIAG
 	if (a.defer_sep) {
 		if (a.window <= 64)
@@ -1494,13 +1495,21 @@ void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 }
 
 // (qt_live 3: both IPv4 lookups through the index; pwide: an index past
-// 2^20 buckets, one lookup direction -- the host takes no other)
+// 2^20 buckets, one lookup direction -- the host takes no other; v6p: the
+// IPv6 lookups in the loop, 1 one direction, 2 both, with one IPv4 direction)
 template <uint32_t FEAT, bool L16>
 void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
 	if constexpr ((FEAT & F_IPV6) != 0)
-		if (a.v6p) {   // (one IPv4 direction, no u32 log: the host's choice)
-			launch_pipeq2<FEAT, L16, false, false, true>(a, grid, dl, s);
+		if (a.v6p) {
+			if (a.v6p == 2 && a.pwide)
+				launch_pipeq2<FEAT, L16, false, true, 2>(a, grid, dl, s);
+			else if (a.v6p == 2)
+				launch_pipeq2<FEAT, L16, false, false, 2>(a, grid, dl, s);
+			else if (a.pwide)
+				launch_pipeq2<FEAT, L16, false, true, 1>(a, grid, dl, s);
+			else
+				launch_pipeq2<FEAT, L16, false, false, 1>(a, grid, dl, s);
 			return;
 		}
 	if (a.qt_live == 3)
@@ -1582,8 +1591,9 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 #define XFG_ALL (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH)
 #define XFG_ALLOW (1u << 5)
 
-// The hit log's count kernel (after a classify that filled a.pbuf / a.pfill;
-// the host may run it on a second stream, overlapped with the next classify)
+// The hit log's count kernel (after a classify that filled a.pbuf / a.pfill,
+// on the same stream: overlapping it with the next classify on a second
+// stream slowed the classify)
 extern "C" int xfg_launch_log_count(const struct xfg_kargs *a, void *stream)
 {
 	if (!a->pbuf)
@@ -1651,10 +1661,38 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 64, true>, PIPE_THREADS(64), dyn)
 				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 128, false>, PIPE_THREADS(128), dyn);
 		} else if (kind == 5) {
+			// (the fewest over the variants a launch may take -- both
+			// directions, the u32 log, the IPv6 lookups: their LDS and
+			// registers differ -- so the persistent grid and the hit-log
+			// slices sized from it hold for whichever one runs)
 			done = true;
-			e = window <= 64
-				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 64, true, true, false, false, false>, QT_THREADS(64), dyn)
-				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeq_kernel<FEAT, 128, false, true, false, true, false>, QT_THREADS(128), dyn);
+			int m = 0;
+			auto q = [&](const void *k, int thr) {
+				int x = 0;
+				const hipError_t r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k, thr, dyn);
+				if (r != hipSuccess)
+					e = r;
+				else if (x > 0 && (m == 0 || x < m))
+					m = x;
+			};
+			if (window <= 64) {
+				q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, false, 0>, QT_THREADS(64));
+				q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, true, false, 0>, QT_THREADS(64));
+				q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, true, 0>, QT_THREADS(64));
+				if constexpr ((FEAT & F_IPV6) != 0) {
+					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, false, 1>, QT_THREADS(64));
+					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, true, 2>, QT_THREADS(64));
+				}
+			} else {
+				q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, false, 0>, QT_THREADS(128));
+				q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, true, false, 0>, QT_THREADS(128));
+				q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, true, 0>, QT_THREADS(128));
+				if constexpr ((FEAT & F_IPV6) != 0) {
+					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, false, 1>, QT_THREADS(128));
+					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, true, 2>, QT_THREADS(128));
+				}
+			}
+			n = m;
 		}
 	}
 	if (done)

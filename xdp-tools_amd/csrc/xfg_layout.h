@@ -87,7 +87,9 @@
 
 #define XFG_QT_SLOTS      16u     /* entries per 32-byte QT bucket */
 #define XFG_QT_BUCKET     32u
+#ifndef XFG_QT_MIN_BITS   /* (A/B builds only: below 17 a remainder loses bits, timing-only) */
 #define XFG_QT_MIN_BITS   17u     /* remainders of at most 15 bits */
+#endif
 #define XFG_QT_LOAD       8u      /* fewer keys per bucket than this on average */
 #define XFG_QT_USED       0x8000u /* an occupied entry */
 #define XFG_QT_OVF_MARK   0x0001u /* entry 15: the bucket overflowed */
@@ -155,8 +157,8 @@ struct xfg_kargs {
 	/* quotient-index kernel with IPv6 keys live (no Ethernet key): every IPv6
 	 * frame goes to the deferred path, the IPv4 lookups through the index */
 	uint32_t v6d;
-	/* ... and (v6p) their lookups in the kernel's loop: exactly one IPv6
-	 * direction live, one IPv4 lookup direction, no u32 hit log */
+	/* ... and (v6p) their lookups in the kernel's loop, with one IPv4
+	 * lookup direction live: 1 = one IPv6 direction live, 2 = both */
 	uint32_t v6p;
 	/* Direct LDS counters: identities below dcnt (all hash maps, gbase[3],
 	 * or the IPv4 map, gbase[1]) are summed per workgroup in LDS; 0 = off */
@@ -173,6 +175,12 @@ struct xfg_kargs {
 	uint32_t *pfill;
 	uint32_t pcap;
 	uint32_t pslices;
+	/* this launch's first slice of each partition (slices pslice0 ..
+	 * pslice0 + grid - 1: the quotient-index kernel's logs of up to
+	 * pslices / grid launches share the buffers, counted together) and
+	 * the count kernel's slices to read (0 .. pcount - 1) */
+	uint32_t pslice0;
+	uint32_t pcount;
 	uint32_t log_hist;
 	/* a partition's local-index range (log_span) beyond one histogram: the
 	 * count kernel takes it in passes of log_hist (one workgroup per

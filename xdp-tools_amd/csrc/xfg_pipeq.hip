@@ -95,7 +95,7 @@ __device__ __forceinline__ uint32_t qt_drain_one(const xfg_kargs &a, const uint3
 	return act;
 }
 
-template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE, bool V6P>
+template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE, uint32_t V6>
 __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
 	static_assert((FEAT & F_IPV4) != 0, "IPv4-key mode needs the IPv4 feature");
@@ -126,10 +126,15 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// bucket lines of the canonical IPv6 table loaded four lanes to a line
 	// (ONE load instruction), moved to the frame's lane through LDS and
 	// matched next iteration; a 17th frame, the zero key and a miss in an
-	// overflowed bucket are deferred
-	static_assert(!V6P || ((FEAT & F_IPV6) != 0 && !BOTH), "IPv6 lookups: one IPv4 direction");
+	// overflowed bucket are deferred.  V6 2 (V6B): both IPv6 directions live
+	// -- a second line per frame, its src key's home bucket, loaded by a
+	// second instruction beside the first and matched after the dst line
+	// only where the dst lookup decided nothing (lookup_verdict_ipv6,
+	// xdpfilt_prog.h:152-165: dst first, the first hit's counter alone)
+	constexpr bool V6P = V6 != 0, V6B = V6 == 2;
+	static_assert(V6 <= 2 && (!V6P || ((FEAT & F_IPV6) != 0 && !BOTH)), "IPv6 lookups: one IPv4 direction");
 	// bucket loads per iteration issued before the windows (L, L6)
-	constexpr uint32_t NL = 2 + (SPEC ? 2 : 0) + (V6P ? 1 : 0);
+	constexpr uint32_t NL = 2 + (SPEC ? 2 : 0) + (V6P ? 1 : 0) + (V6B ? 1 : 0);
 	static_assert(D == 2 || (D == 3 && LAG == 2), "window depth: 2, or 3 with a bucket lag of 2");
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	constexpr uint32_t QTAG = CT_QTAG;   // tag bit: a QT slot (hit log), not a counter identity
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
 	__shared__ uint32_t s_lh[XFG_LOG_PARTS];
 	__shared__ unsigned long long s_stats[6];
-	__shared__ uint32_t s6b[V6P ? NW * 16 : 1];   // (V6P) a tile's IPv6 home buckets, by rank
+	__shared__ uint32_t s6b[V6P ? NW * (V6B ? 32 : 16) : 1];   // (V6P) a tile's IPv6 home buckets, by rank (V6B: + src)
 	__shared__ u32x4 s6l[V6P ? NW * 64 : 1];      // (V6P) their lines, four lanes each
 	extern __shared__ uint32_t s_dyn[];
 
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const uint64_t b6base = V6P ? rfl64((uint64_t)(uintptr_t)a.t6.buckets) : 0;
 	const uint32_t nb6 = V6P ? rfl(a.t6.nbuckets) : 0u, seed6 = V6P ? rfl(a.t6.seed) : 0u;
 	const bool md6 = V6P && a.t6.max_disp != 0, k6live = V6P && a.t6.count != 0;
-	const bool d6 = (a.t6.fmask & M_DST) == M_DST;
+	const bool d6 = V6B || (a.t6.fmask & M_DST) == M_DST;
 	const uint32_t m6 = d6 ? M_DST : M_SRC, gb6 = rfl(a.gbase[1]);
 	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
 	cn.init(a, tid, NT);
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	auto ownp = [&](uint32_t j) { return XFG_QT_OWNC ? (uint32_t)wv * PPW + j : j * NW + (uint32_t)wv; };
 	const uint32_t wc_p = ownp((uint32_t)lane);
 	uint32_t wc_fl = 0;
-	const uint64_t wc_slice0 = (uint64_t)blockIdx.x * a.pcap;
+	const uint64_t wc_slice0 = (uint64_t)(blockIdx.x + a.pslice0) * a.pcap;
 	const uint64_t wc_pstep = (uint64_t)a.pslices * a.pcap;
 	__syncthreads();
 
@@ -316,14 +321,32 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const uint32_t nt = (n + 63) / 64;
 	const uint32_t first = blockIdx.x * NW + wv;
 	const uint32_t step = gridDim.x * NW;
-	uint32_t st_c0 = 0, st_c1 = 0, st_c2 = 0, st_b0 = 0, st_b1 = 0, st_b2 = 0;
+	// xdp_stats_record_action (headers/xdp/xdp_stats_kern.h): per lane, the
+	// packets of each action in 10-bit fields of one word and their bytes
+	// in 21-bit fields of one double word -- a shift-add each per tile,
+	// the field chosen by the action (ABORTED, DROP, PASS; any other --
+	// a deferred or absent packet -- into the top bits, discarded) --
+	// folded into per-lane totals before a field can overflow (every
+	// st_cap tiles: 1023 packets, 2^21 - 1 bytes of the longest length)
+	uint32_t st_pk = 0, st_n = 0, st_c[3] = { 0, 0, 0 }, st_b[3] = { 0, 0, 0 };
+	uint64_t st_bpk = 0;
+	const uint32_t st_cap = rfl(min(1023u, 0x1fffffu / max(min(a.stride ? a.stride : 65535u, 65535u), 1u)));
+	auto st_fold = [&]() {
+#pragma unroll
+		for (int k = 0; k < 3; k++) {
+			st_c[k] += (st_pk >> (10 * k)) & 1023u;
+			st_b[k] += (uint32_t)(st_bpk >> (21 * k)) & 0x1fffffu;
+		}
+		st_pk = 0;
+		st_bpk = 0;
+		st_n = 0;
+	};
 	auto stat = [&](uint32_t act, uint32_t len) {
-		st_c0 += (uint32_t)__popcll(__ballot(act == A_ABORTED));
-		st_c1 += (uint32_t)__popcll(__ballot(act == A_DROP));
-		st_c2 += (uint32_t)__popcll(__ballot(act == A_PASS));
-		st_b0 += pick(act == A_ABORTED, len, 0u);
-		st_b1 += pick(act == A_DROP, len, 0u);
-		st_b2 += pick(act == A_PASS, len, 0u);
+		const uint32_t f = min(act, 3u);
+		st_pk += 1u << (f * 10);
+		st_bpk += (uint64_t)len << (f * 21);
+		if (++st_n == st_cap)
+			st_fold();
 	};
 	uint32_t ndef = 0;
 
@@ -390,9 +413,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		uint32_t k6[4], b6, r6;
 		bool s6;
 		u32x4 c6;
+		// (V6B) the src key, its home bucket, this lane's quarter of its line
+		uint32_t k6s[V6B ? 4 : 1], b6s;
+		u32x4 c6s;
 	};
 	RSt stA = { 0, 0, pk3(A_NONE, XFG_PORT_TAB, 0), CT_NONE, 0, 0, false, { 0, 0, 0, 0 }, { 0, 0, 0, 0 },
-		    { 0, 0, 0, 0 }, { 0, 0, 0, 0 }, { 0, 0, 0, 0 }, 0, 0, false, { 0, 0, 0, 0 } };
+		    { 0, 0, 0, 0 }, { 0, 0, 0, 0 }, { 0, 0, 0, 0 }, 0, 0, false, { 0, 0, 0, 0 }, {}, 0, { 0, 0, 0, 0 } };
 	RSt stB = stA;
 	// (both directions: the src key's entry and bucket from P; tile k-1's
 	// state after its dst lookup, for R2 next iteration; its src bucket)
@@ -420,7 +446,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 		return (w[7] >> 16) == XFG_QT_OVF_MARK;
 	};
-	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen, RSt &rs) __attribute__((always_inline)) {
+	// (wcf: this iteration moves completed hit-log chunks -- every other one:
+	// a ring of WR entries takes two iterations' hits with room to spare)
+	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen, RSt &rs, bool wcf) __attribute__((always_inline)) {
 		const uint32_t tP = first + k * step;
 		const bool vP = tP < nt;
 		const bool vR = k >= LAG && tP - LAG * step < nt;
@@ -487,22 +515,42 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				__builtin_amdgcn_wave_barrier();
 				s6l[wv * 64 + lane] = rs.c6;
 				__builtin_amdgcn_wave_barrier();
-				bool f6 = false, o6 = false;
-				uint32_t i6 = 0;
-				if (rs.s6) {
+				// this lane's frame's line (rank r6, lanes 4 r6 .. + 3) against
+				// key k: the key found with the mask's flags, a miss the
+				// overflow bit leaves undecided, the slot
+				auto m6line = [&](const uint32_t (&k)[4], uint32_t m, bool &f, bool &o, uint32_t &ix) {
 					const u32x4 *ln = &s6l[wv * 64 + rs.r6 * 4];
 					const u32x4 q0 = ln[0], q1 = ln[1], q2 = ln[2], q3 = ln[3];
-					const bool e0 = (q0.x == rs.k6[0]) & (q0.y == rs.k6[1]) & (q0.z == rs.k6[2]) & (q0.w == rs.k6[3]);
-					const bool e1 = (q1.x == rs.k6[0]) & (q1.y == rs.k6[1]) & (q1.z == rs.k6[2]) & (q1.w == rs.k6[3]);
-					const bool e2 = (q2.x == rs.k6[0]) & (q2.y == rs.k6[1]) & (q2.z == rs.k6[2]) & (q2.w == rs.k6[3]);
-					i6 = pick(e0, 0u, pick(e1, 1u, 2u));
-					const uint32_t fl = (q3.x >> (8 * i6)) & 0xff;
-					f6 = (e0 | e1 | e2) & ((fl & m6) == m6);
-					o6 = !(e0 | e1 | e2) & ((q3.w & XFG_META_OVERFLOW) != 0) & md6;
-				}
+					const bool e0 = (q0.x == k[0]) & (q0.y == k[1]) & (q0.z == k[2]) & (q0.w == k[3]);
+					const bool e1 = (q1.x == k[0]) & (q1.y == k[1]) & (q1.z == k[2]) & (q1.w == k[3]);
+					const bool e2 = (q2.x == k[0]) & (q2.y == k[1]) & (q2.z == k[2]) & (q2.w == k[3]);
+					ix = pick(e0, 0u, pick(e1, 1u, 2u));
+					const uint32_t fl = (q3.x >> (8 * ix)) & 0xff;
+					f = (e0 | e1 | e2) & ((fl & m) == m);
+					o = !(e0 | e1 | e2) & ((q3.w & XFG_META_OVERFLOW) != 0) & md6;
+				};
+				bool f6 = false, o6 = false;
+				uint32_t i6 = 0;
+				if (rs.s6)
+					m6line(rs.k6, m6, f6, o6, i6);
 				x_act = pick(f6, HIT, pick(o6, A_DEFER, x_act));
 				x_tag = pick(f6, gb6 + rs.b6 * XFG_SLOTS_V6 + i6, pick(o6, CT_NONE, x_tag));
 				x_ps = pick(f6 | o6, XFG_PORT_TAB, x_ps);
+				if constexpr (V6B) {
+					// the src line where the dst key decided nothing (found
+					// without the dst flag, or absent from a bucket that
+					// never overflowed)
+					__builtin_amdgcn_wave_barrier();
+					s6l[wv * 64 + lane] = rs.c6s;
+					__builtin_amdgcn_wave_barrier();
+					bool fs = false, os = false;
+					uint32_t is = 0;
+					if (rs.s6 & !f6 & !o6)
+						m6line(rs.k6s, M_SRC, fs, os, is);
+					x_act = pick(fs, HIT, pick(os, A_DEFER, x_act));
+					x_tag = pick(fs, gb6 + rs.b6s * XFG_SLOTS_V6 + is, pick(os, CT_NONE, x_tag));
+					x_ps = pick(fs | os, XFG_PORT_TAB, x_ps);
+				}
 			}
 			if constexpr (SPEC) {   // the src lookup, its bucket loaded beside the dst one
 				const bool need = rs.sel & !found & !defer;
@@ -563,7 +611,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				ndef += (uint32_t)__popcll(dm);
 			}
 		}
-		if (vW && logon)
+		if (vW && logon && wcf)
 			wc_flush();
 
 		PMARK("S");
@@ -675,19 +723,32 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				// row dword), its home bucket, its rank among the tile's
 				// lookups; ranks below 16 post their bucket for L6
 				const bool k6 = valid & !r.defer & r.v6ok & k6live;
-				uint32_t w6[4];
+				uint32_t w6[4], ws[4];
 #pragma unroll
-				for (int i = 0; i < 4; i++)
+				for (int i = 0; i < 4; i++) {
 					w6[i] = d6 ? __builtin_amdgcn_alignbyte(rowd(10 + i), rowd(9 + i), 2)
 						   : __builtin_amdgcn_alignbyte(rowd(6 + i), rowd(5 + i), 2);
-				const bool z6 = (w6[0] | w6[1] | w6[2] | w6[3]) == 0;   // (slot nslots: deferred)
+					ws[i] = __builtin_amdgcn_alignbyte(rowd(6 + i), rowd(5 + i), 2);   // (V6B: saddr)
+				}
+				// (the zero key lives in slot nslots: deferred; V6B: either)
+				const bool z6 = (w6[0] | w6[1] | w6[2] | w6[3]) == 0 ||
+						(V6B && (ws[0] | ws[1] | ws[2] | ws[3]) == 0);
 				const unsigned long long bm6 = __ballot(k6 & !z6);
 				const uint32_t rk = lanes_below(bm6);
 				const bool sel6 = k6 & !z6 & (rk < 16);
 				def6 = k6 & !sel6;
 				const uint32_t hb6 = xfg_home(xfg_hash_v6(w6[0], w6[1], w6[2], w6[3], seed6), nb6);
 				if (sel6)
-					s6b[wv * 16 + rk] = hb6;
+					s6b[wv * (V6B ? 32 : 16) + rk] = hb6;
+				if constexpr (V6B) {
+					const uint32_t hs = xfg_home(xfg_hash_v6(ws[0], ws[1], ws[2], ws[3], seed6), nb6);
+					if (sel6)
+						s6b[wv * 32 + 16 + rk] = hs;
+#pragma unroll
+					for (int i = 0; i < 4; i++)
+						rs.k6s[i] = ws[i];
+					rs.b6s = hs;
+				}
 				n6 = min((uint32_t)__popcll(bm6), 16u);
 #pragma unroll
 				for (int i = 0; i < 4; i++)
@@ -749,9 +810,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			// line of bucket 0)
 			__builtin_amdgcn_wave_barrier();
 			const uint32_t j = (uint32_t)lane >> 2;
-			const uint32_t bb = j < n6 ? s6b[wv * 16 + j] : 0u;
+			const uint32_t bb = j < n6 ? s6b[wv * (V6B ? 32 : 16) + j] : 0u;
 			rs.c6 = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(
 				b6base + (uint64_t)bb * XFG_BUCKET_BYTES + ((uint32_t)lane & 3) * 16);
+			if constexpr (V6B) {   // (the src lines: a second instruction, the same shape)
+				const uint32_t bs = j < n6 ? s6b[wv * 32 + 16 + j] : 0u;
+				rs.c6s = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(
+					b6base + (uint64_t)bs * XFG_BUCKET_BYTES + ((uint32_t)lane & 3) * 16);
+			}
 		}
 
 		PMARK("I");
@@ -785,20 +851,20 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		constexpr uint32_t u = decltype(uc)::value;
 		RSt &rs = (LAG == 2 && (u & 1)) ? stB : stA;
 		if constexpr (u % D == 0)
-			iteration(k, preA, lenA, rs);
+			iteration(k, preA, lenA, rs, u % 2 == 0);
 		else if constexpr (u % D == 1)
-			iteration(k, preB, lenB, rs);
+			iteration(k, preB, lenB, rs, u % 2 == 0);
 		else if constexpr (D == 3)
-			iteration(k, preC, lenC, rs);
+			iteration(k, preC, lenC, rs, u % 2 == 0);
 	};
 	if constexpr (D == 2) {
 		uint32_t k = 0;
 		for (; k + 1 < iters; k += 2) {
-			iteration(k, preA, lenA, stA);
-			iteration(k + 1, preB, lenB, LAG == 2 ? stB : stA);
+			iteration(k, preA, lenA, stA, true);
+			iteration(k + 1, preB, lenB, LAG == 2 ? stB : stA, false);
 		}
 		if (k < iters)
-			iteration(k, preA, lenA, stA);
+			iteration(k, preA, lenA, stA, true);
 	} else {
 		// whole bodies unguarded (exact wait counts), then the rest guarded
 		uint32_t k = 0;
@@ -846,15 +912,18 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		stat(act, len);
 	}
 
-	const uint32_t vb[3] = { st_b0, st_b1, st_b2 }, vc[3] = { st_c0, st_c1, st_c2 };
+	st_fold();
 #pragma unroll
 	for (int kk = 0; kk < 3; kk++) {
-		unsigned long long x = vb[kk];
+		unsigned long long x = st_b[kk];
+		uint32_t c = st_c[kk];
 #pragma unroll
-		for (int o = 32; o > 0; o >>= 1)
+		for (int o = 32; o > 0; o >>= 1) {
 			x += __shfl_xor(x, o);
-		if (lane == 0 && vc[kk]) {
-			atomicAdd(&s_stats[2 * kk], (unsigned long long)vc[kk]);
+			c += __shfl_xor(c, o);
+		}
+		if (lane == 0 && c) {
+			atomicAdd(&s_stats[2 * kk], (unsigned long long)c);
 			atomicAdd(&s_stats[2 * kk + 1], x);
 		}
 	}
@@ -866,13 +935,43 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// position past a slice goes to the counter cache, flushed below
 	if (a.pbuf && !(dg & 16)) {
 		const uint32_t hd = (uint32_t)lane < PPW ? s_hd[2 * wc_p] : 0u;
-		for (uint32_t j = 0; j < PPW; j++) {
-			const uint32_t fl = __builtin_amdgcn_readlane(wc_fl, j);
-			const uint32_t h = __builtin_amdgcn_readlane(hd, j);
-			wc_move(j, fl, h - fl);
+		// (every position within its slice -- the usual case: two rings
+		// per instruction, 8 bytes a lane, one LDS read and one store each
+		// for the lanes whose entries are consecutive tickets; a ring holds
+		// tickets [fl, h) at slots t & (WR - 1), so slot s carries ticket
+		// fl + ((s - fl) & (WR - 1)), 8-byte aligned in the slice)
+		constexpr uint32_t EPL = 8 / sizeof(ring_t);
+		if (WR * sizeof(ring_t) == 256 && __ballot(((uint32_t)lane < PPW) & (hd > a.pcap)) == 0) {
+			const uint32_t half = (uint32_t)lane >> 5, s0 = ((uint32_t)lane & 31) * EPL;
+#pragma unroll 4
+			for (uint32_t j = 0; j < PPW; j += 2) {
+				const uint32_t fl = half ? __builtin_amdgcn_readlane(wc_fl, j + 1) : __builtin_amdgcn_readlane(wc_fl, j);
+				const uint32_t h = half ? __builtin_amdgcn_readlane(hd, j + 1) : __builtin_amdgcn_readlane(hd, j);
+				const uint32_t p = ownp(j + half);
+				const uint64_t v = *reinterpret_cast<const uint64_t *>(&s_ring[p * WR + s0]);
+				const uint32_t t0 = fl + ((s0 - fl) & (WR - 1));
+				ring_t *sl = reinterpret_cast<ring_t *>(a.pbuf) + p * wc_pstep + wc_slice0;
+				if (t0 + EPL - 1 == fl + ((s0 + EPL - 1 - fl) & (WR - 1)) && t0 + EPL <= h) {
+					*reinterpret_cast<__attribute__((address_space(1))) uint64_t *>((uintptr_t)(sl + t0)) = v;
+				} else {
+#pragma unroll
+					for (uint32_t i = 0; i < EPL; i++) {
+						const uint32_t t = fl + ((s0 + i - fl) & (WR - 1));
+						if (t < h)
+							*reinterpret_cast<__attribute__((address_space(1))) ring_t *>((uintptr_t)(sl + t)) =
+								(ring_t)(v >> (i * 8 * sizeof(ring_t)));
+					}
+				}
+			}
+		} else {
+			for (uint32_t j = 0; j < PPW; j++) {
+				const uint32_t fl = __builtin_amdgcn_readlane(wc_fl, j);
+				const uint32_t h = __builtin_amdgcn_readlane(hd, j);
+				wc_move(j, fl, h - fl);
+			}
 		}
 		if ((uint32_t)lane < PPW)
-			gst32(a.pfill + (uint64_t)wc_p * a.pslices + blockIdx.x, hd);
+			gst32(a.pfill + (uint64_t)wc_p * a.pslices + a.pslice0 + blockIdx.x, hd);
 	}
 	__syncthreads();
 	if (tid < 6 && s_stats[tid])
