@@ -90,6 +90,10 @@ def parse():
     # launcher tests (CPU only): a rank body that touches no GPU
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--stub-stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--stub-reduce-stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--reduce-timeout", type=float, default=REDUCE_TIMEOUT_S,
+                    help="seconds before the readout all-reduce counts as stalled")
     return ap.parse_args()
 
 
@@ -190,28 +194,18 @@ def main():
     # line and never keeps the line from being printed)
     reduce_ms, reduce_err, reduce_stuck = None, None, False
     if world > 1:
-        import threading
         uid = [G.Filter.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        box = {}
 
         def _reduce():
-            try:
-                f.comm_init(world, rank, uid[0])
-                f.sync()
-                tr = time.perf_counter()
-                f.comm_allreduce()
-                f.sync()
-                box["ms"] = (time.perf_counter() - tr) * 1e3
-            except Exception as e:  # reported, not fatal to the measurement
-                box["err"] = repr(e)
+            f.comm_init(world, rank, uid[0])
+            f.sync()
+            tr = time.perf_counter()
+            f.comm_allreduce()
+            f.sync()
+            return (time.perf_counter() - tr) * 1e3
 
-        th = threading.Thread(target=_reduce, daemon=True)
-        th.start()
-        th.join(REDUCE_TIMEOUT_S)
-        reduce_stuck = th.is_alive()
-        reduce_ms = box.get("ms")
-        reduce_err = "timed out" if reduce_stuck else box.get("err")
+        reduce_ms, reduce_err, reduce_stuck = watched_reduce(_reduce, args.reduce_timeout)
 
     # ---- achievable streaming-read peak on this device (same 1 GiB buffer)
     peak_meas_ms = f.stream_read_timed(d_data.ptr, n * stride, 5)
@@ -321,6 +315,28 @@ def main():
         dist.destroy_process_group()
 
 
+def watched_reduce(fn, timeout):
+    """The readout all-reduce on a watchdog thread (fn returns its ms):
+    (ms, error, stuck) -- a failure or a stall is reported in the line,
+    never keeps it from being printed, and a stall ends the rank with
+    exit status 3 after the line (the per-CPU counter sum at readout,
+    xdp-filter/xdp-filter.c:93-103)."""
+    import threading
+    box = {}
+
+    def run():
+        try:
+            box["ms"] = fn()
+        except Exception as e:  # reported, not fatal to the measurement
+            box["err"] = repr(e)
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(timeout)
+    stuck = th.is_alive()
+    return box.get("ms"), ("timed out" if stuck else box.get("err")), stuck
+
+
 def init_gloo():
     """The CPU process group (barriers, the max over ranks); gloo's connect
     message goes to stderr, so that stdout carries only the JSON line."""
@@ -349,9 +365,15 @@ def max_over_ranks(dist, wall):
 
 def stub_rank(args):
     """Launcher test body (no GPU): the rank's barriers and max-over-ranks
-    wall time over gloo, and rank 0's line with n_gpus = world size."""
+    wall time over gloo, the readout reduce on its watchdog (a gloo sum of
+    the ranks' counter stand-ins in place of RCCL), and rank 0's line with
+    n_gpus = world size, every rank's LOCAL_RANK (the device it would bind)
+    and reduce_ms / reduce_error.  --stub-stall-rank R: rank R never
+    finishes its timed region (the launcher's --rank-timeout kills the run);
+    --stub-reduce-stall-rank R: rank R's reduce never completes."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     if rank == args.stub_fail_rank:
         return 3
     dist = init_gloo() if world > 1 else None
@@ -359,14 +381,42 @@ def stub_rank(args):
         dist.barrier()
     t1 = time.perf_counter()
     time.sleep(0.01 * (rank + 1))
+    if rank == args.stub_stall_rank:
+        time.sleep(3600)
     if dist is not None:
         dist.barrier()
     wall = max_over_ranks(dist, time.perf_counter() - t1)
+    locals_ = [local]
+    reduce_ms, reduce_err, stuck = None, None, False
+    if dist is not None:
+        import torch
+        locals_ = [None] * world
+        dist.all_gather_object(locals_, local)
+
+        def _reduce():
+            if rank == args.stub_reduce_stall_rank:
+                time.sleep(3600)
+            t = torch.full((4,), rank + 1, dtype=torch.int64)
+            tr = time.perf_counter()
+            dist.all_reduce(t)
+            if int(t[0]) != world * (world + 1) // 2:
+                raise RuntimeError(f"reduce sum {int(t[0])}")
+            return (time.perf_counter() - tr) * 1e3
+
+        reduce_ms, reduce_err, stuck = watched_reduce(_reduce, args.reduce_timeout)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "Mpps", "n_gpus": world,
-                          "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": round(wall * 1e3 / max(args.steps, 1), 4),
-                          "stub": True}), flush=True)
+        line = {"metric": METRIC, "value": 0.0, "unit": "Mpps", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(wall * 1e3 / max(args.steps, 1), 4),
+                "local_ranks": locals_, "stub": True}
+        if reduce_ms is not None:
+            line["reduce_ms"] = round(reduce_ms, 3)
+        if reduce_err is not None:
+            line["reduce_error"] = reduce_err
+        print(json.dumps(line), flush=True)
+    if stuck:
+        sys.stdout.flush()
+        os._exit(3)
     if dist is not None:
         dist.destroy_process_group()
     return 0

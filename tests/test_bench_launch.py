@@ -48,3 +48,37 @@ def test_single_gpu_runs_in_process():
     p = _run("--gpus", "1")
     assert p.returncode == 0, p.stderr
     assert json.loads(p.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+
+
+def test_eight_rank_self_launch_binds_local_ranks_and_reduces():
+    """The driver's 8-GPU run, rehearsed on the CPU: eight fresh ranks, each
+    with its own LOCAL_RANK (the device it binds), one line from rank 0,
+    the readout reduce (gloo here, RCCL on the GPUs) summing every rank's
+    counters and reported as reduce_ms."""
+    p = _run("--gpus", "8", timeout=240)
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8
+    assert rec["local_ranks"] == list(range(8))
+    assert "reduce_error" not in rec and rec["reduce_ms"] >= 0
+    # the max over ranks: rank 7 sleeps 80 ms in its timed region
+    assert rec["ms_per_step"] >= 80.0 / 3 * 0.9
+
+
+def test_eight_ranks_one_stalled_fails_the_run():
+    p = _run("--gpus", "8", "--stub-stall-rank", "5", "--rank-timeout", "20", timeout=240)
+    assert p.returncode == 124, (p.returncode, p.stderr)
+    assert "stalled" in p.stderr
+
+
+def test_eight_ranks_stalled_reduce_is_reported():
+    """A reduce that never completes on one rank: rank 0 still prints its
+    line, with reduce_error, and the run exits non-zero (status 3)."""
+    p = _run("--gpus", "8", "--stub-reduce-stall-rank", "3", "--reduce-timeout", "3",
+             timeout=240)
+    assert p.returncode == 3, (p.returncode, p.stderr)
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.strip()][-1])
+    assert rec["n_gpus"] == 8 and rec["reduce_error"] == "timed out"
+    assert "reduce_ms" not in rec

@@ -506,17 +506,20 @@ def test_qt_hits_concentrated_in_few_log_partitions(G, stride):
 def test_qt_with_ipv6_rules(G, variant, stride, dirs6):
     """IPv6 rules beside the IPv4 map (C5's shape, no Ethernet rule): the
     index kernel still takes the batch and the IPv4 lookups stay on the
-    index.  With one IPv6 direction live (dst or src rules) the kernel looks
-    the IPv6 keys up in its loop -- up to 16 frames a tile through their home
-    bucket lines, the rest and the misses in overflowed buckets deferred;
-    with both live every IPv6 frame takes the deferred walk over the
-    canonical tables (dst then src, xdpfilt_prog.h:152-165)."""
+    index.  The kernel looks the IPv6 keys up in its loop -- up to 16
+    frames a tile through their home bucket lines, the rest and the misses
+    in overflowed buckets deferred -- with one direction live (dst or src
+    rules: one line a frame) or both (src,dst rule sets, V6B: the src line
+    beside the dst one, matched only where the dst key decided nothing,
+    dst then src, xdpfilt_prog.h:152-165).  For both, frames carry ruled
+    sources, and destinations ruled for the source direction only (found,
+    CHECK_MAP's mask fails, the src key decides)."""
     rng = np.random.default_rng(101)
     rules, v4, ports = one_direction_rules(102, 20000, 2)
     v6 = X.rand_keys(103, 4000, 16)
     rules.v6_keys = v6
     if dirs6 == "both":
-        f6 = np.where(rng.random(len(v6)) < 0.5, 2, 1).astype(np.uint64)
+        f6 = rng.choice(np.array([1, 2, 3], np.uint64), len(v6))
     else:
         f6 = np.full(len(v6), 2 if dirs6 == "dst" else 1, np.uint64)
     f6[rng.random(len(v6)) < 0.1] |= 4
@@ -527,6 +530,14 @@ def test_qt_with_ipv6_rules(G, variant, stride, dirs6):
     # a run of IPv6 frames only: whole tiles with more than 16 IPv6 lookups
     fr = d1.reshape(-1, stride)
     six = np.nonzero((fr[:, 12] == 0x86) & (fr[:, 13] == 0xdd))[0]
+    if dirs6 == "both":
+        # ruled sources on a third of the IPv6 frames; on a sixth, a
+        # destination ruled for the source direction only
+        srcs = six[::3]
+        fr[srcs, 22:38] = v6[rng.integers(0, len(v6), len(srcs))]
+        only_src = v6[(f6 & 3) == 1]
+        dsts = six[1::6]
+        fr[dsts, 38:54] = only_src[rng.integers(0, len(only_src), len(dsts))]
     pick = six[np.arange(1 << 13) % len(six)]
     d3, l3 = fr[pick].reshape(-1), l1[pick]
     data = np.concatenate([d1, d2, d3])

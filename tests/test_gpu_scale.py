@@ -57,10 +57,10 @@ def _c3_rules():
     return rules, v4, ports
 
 
-def _check(G, rules, data, lens, cap=1_000_000):
+def _check(G, rules, data, lens, cap=1_000_000, **kw):
     ov, orules, ost = X.run_oracle(X.VARIANT_FEATURES["xdpfilt_dny_all"], data, lens, rules,
                                    stride=64, nthreads=_threads())
-    f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=cap)
+    f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=cap, **kw)
     f.load_rules(rules)
     v = f.run(data, lens, stride=64)
     assert f.last_path() == f.PATH_QT   # the quotient index (1M dst rules)
@@ -102,13 +102,29 @@ def test_c3_skewed_hits_overfill_log_partitions_2p25(G):
 
 
 @pytest.mark.timeout(900)
-def test_wide_hit_log_9m_rules_2p25(G):
+@pytest.mark.parametrize("v6", ["none", "both"])
+def test_wide_hit_log_9m_rules_2p25(G, v6):
+    """... and (v6 "both") 200k IPv6 rules, dst, src and src|dst, beside
+    them: the IPv6 lookups in the index kernel's loop with the u32 log
+    (VERDICT r4 item 3), a third of the IPv6 frames from a ruled source."""
     n4 = 9_000_000
     v4 = X.rand_keys(41, int(n4 * 1.02) + 16, 4)[:n4]
     rules = X.RuleSet()
     rules.v4_keys = v4
     rules.v4_vals = np.full(len(v4), 2, np.uint64)
     n = 1 << 25
-    data, lens = X.gen_workload(42, 3, n, 64, v4=v4, dst_permille=600, bad_permille=10)
-    ov, _ = _check(G, rules, data, lens.astype(np.uint16), cap=n4)
+    kw = {}
+    v6k = None
+    if v6 == "both":
+        rng = np.random.default_rng(43)
+        v6k = X.rand_keys(44, 200_000, 16)
+        rules.v6_keys = v6k
+        rules.v6_vals = rng.choice(np.array([1, 2, 3], np.uint64), len(v6k))
+        kw = {"ipv6_capacity": 200_000}
+    data, lens = X.gen_workload(42, 3, n, 64, v4=v4, v6=v6k, dst_permille=600, bad_permille=10)
+    if v6k is not None:
+        fr = data.reshape(-1, 64)
+        six = np.nonzero((fr[:, 12] == 0x86) & (fr[:, 13] == 0xdd))[0][::3]
+        fr[six, 22:38] = v6k[np.arange(len(six)) * 7919 % len(v6k)]
+    ov, _ = _check(G, rules, data, lens.astype(np.uint16), cap=n4, **kw)
     assert (ov == 2).sum() > n // 3
