@@ -1337,14 +1337,23 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 				atomicAdd(&hist[l1], 1u);
 		}
 	};
-	for (uint32_t s0 = a.pwide ? S : w; s0 < S; s0 += NWV * U) {
-		u32x4 v[U];
+	// (two rounds of U slices in flight: the next round's loads issued
+	// before this round's LDS atomics -- with the logs of several launches
+	// a wave takes dozens of slices)
+	auto ld = [&](uint32_t s0, u32x4 (&d)[U]) {
 #pragma unroll
 		for (uint32_t u = 0; u < U; u++) {
 			const uint32_t sl = s0 + u * NWV;
 			const u32x4 *e = (const u32x4 *)(base + (uint64_t)sl * cap);
-			v[u] = sl < S && s_fill[sl] ? __builtin_nontemporal_load(e + lane) : u32x4{ 0, 0, 0, 0 };
+			d[u] = sl < S && s_fill[sl] ? __builtin_nontemporal_load(e + lane) : u32x4{ 0, 0, 0, 0 };
 		}
+	};
+	u32x4 v[U], nx[U];
+	if (!a.pwide && w < S)
+		ld(w, v);
+	for (uint32_t s0 = a.pwide ? S : w; s0 < S; s0 += NWV * U) {
+		if (s0 + NWV * U < S)
+			ld(s0 + NWV * U, nx);
 #pragma unroll
 		for (uint32_t u = 0; u < U; u++) {
 			const uint32_t sl = s0 + u * NWV;
@@ -1359,6 +1368,9 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 			for (uint32_t i = 512 + lane * 8; i < np; i += 512)
 				add8(__builtin_nontemporal_load(e + i / 8), i, np);
 		}
+#pragma unroll
+		for (uint32_t u = 0; u < U; u++)
+			v[u] = nx[u];
 	}
 	__syncthreads();
 #pragma unroll

@@ -70,6 +70,21 @@
 #ifndef XFG_QT_WC_R128   /* ... 128-byte windows (4 waves: two workgroups a CU) */
 #define XFG_QT_WC_R128 32
 #endif
+#ifndef XFG_QT_ORDER     /* 1: W after L -- the bucket loads issued before the verdict / log work */
+#define XFG_QT_ORDER 0
+#endif
+#ifndef XFG_QT_VST       /* 1: a tile's verdict bytes stored at the top of the next iteration */
+#define XFG_QT_VST 0
+#endif
+#ifndef XFG_QT_VGRP      /* 1: a wave's tiles in runs of 4 consecutive tiles, verdicts stored 256 B at once */
+#define XFG_QT_VGRP 0
+#endif
+#ifndef XFG_QT_PADV      /* (A/B only: extra VALU / SALU instructions per tile, to price one) */
+#define XFG_QT_PADV 0
+#endif
+#ifndef XFG_QT_PADS
+#define XFG_QT_PADS 0
+#endif
 
 namespace {
 
@@ -168,6 +183,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	__shared__ unsigned long long s_stats[6];
 	__shared__ uint32_t s6b[V6P ? NW * (V6B ? 32 : 16) : 1];   // (V6P) a tile's IPv6 home buckets, by rank (V6B: + src)
 	__shared__ u32x4 s6l[V6P ? NW * 64 : 1];      // (V6P) their lines, four lanes each
+	constexpr uint32_t G = XFG_QT_VGRP ? 4u : 1u;   // tiles per run (VGRP)
+	__shared__ uint32_t s_vb[G > 1 ? NW * 64 : 1];   // (VGRP) a run's verdict bytes, per wave
 	extern __shared__ uint32_t s_dyn[];
 
 #ifdef XFG_DIAG
@@ -203,6 +220,74 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const bool md6 = V6P && a.t6.max_disp != 0, k6live = V6P && a.t6.count != 0;
 	const bool d6 = V6B || (a.t6.fmask & M_DST) == M_DST;
 	const uint32_t m6 = d6 ? M_DST : M_SRC, gb6 = rfl(a.gbase[1]);
+	const uint32_t n = (uint32_t)a.n;
+	const uint32_t nt = (n + 63) / 64;
+	const uint32_t first = blockIdx.x * NW + wv;
+	const uint32_t step = gridDim.x * NW;
+	// iteration kk's tile: every step-th tile (G 1), or runs of G consecutive
+	// tiles, every step-th run (G 4: a run's 256 verdict bytes contiguous)
+	auto tileOf = [&](uint32_t kk) -> uint32_t {
+		return G == 1 ? first + kk * step : (first + (kk / G) * step) * G + (kk % G);
+	};
+	// windows + lengths of tile t (clamped to the last tile): CPP + 1 loads,
+	// always issued
+	// (the length width is a template parameter: one load of a fixed kind,
+	// so the compiler's wait counts stay exact across the loop)
+	constexpr uint32_t lsh = L16 ? 1u : 2u;
+	typedef typename std::conditional<L16, uint16_t, uint32_t>::type len_t;
+	const uint64_t lb = rfl64((uint64_t)(uintptr_t)a.lens);
+	auto ld_len = [](uint64_t p) {
+		const auto *q = reinterpret_cast<const __attribute__((address_space(1))) len_t *>(p);
+#if XFG_QT_NTLEN   /* (A/B: the lengths streamed like the windows) */
+		return __builtin_nontemporal_load(q);
+#else
+		return *q;
+#endif
+	};
+	// (a whole tile -- every one but a ragged last -- takes a uniform branch
+	// with no per-lane clamps: a scalar tile base and per-lane offsets that
+	// do not change from tile to tile; the same loads either way)
+	auto issue = [&](uint32_t t, u32x4 (&pre)[CPP], len_t &plen) {
+		t = t < nt ? t : nt - 1;
+		const uint32_t base = t * 64;
+		const uint32_t rem = n - base >= 64 ? 64u : n - base;
+		if (rem == 64) {
+			const uint8_t *tb = a.data + (uint64_t)base * (DENSE ? W : a.stride);
+#pragma unroll
+			for (int it = 0; it < CPP; it++) {
+				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
+				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
+							 : reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
+				pre[it] = __builtin_nontemporal_load(src);
+			}
+			plen = ld_len(lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
+		} else {
+#pragma unroll
+			for (int it = 0; it < CPP; it++) {
+				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
+				const uint32_t q = pk < rem ? pk : 0u;
+				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + (q * CPP + sub)
+							 : reinterpret_cast<const u32x4 *>(a.data + (uint64_t)(base + q) * a.stride + sub * 16);
+				pre[it] = __builtin_nontemporal_load(src);
+			}
+			const uint64_t la = lb + ((uint64_t)(base + ((uint32_t)lane < rem ? lane : 0u)) << lsh);
+			plen = ld_len(la);
+		}
+	};
+	// the first tiles' windows in flight before the workgroup's LDS set-up
+	// (counters, port image, log rings) and its barrier
+	u32x4 preA[CPP], preB[CPP], preC[D == 3 ? CPP : 1];
+	len_t lenA = 0, lenB = 0, lenC = 0;
+	if (nt) {
+		issue(tileOf(0), preA, lenA);
+		__builtin_amdgcn_sched_barrier(0);
+		issue(tileOf(1), preB, lenB);
+		__builtin_amdgcn_sched_barrier(0);
+		if constexpr (D == 3) {
+			issue(tileOf(2), preC, lenC);
+			__builtin_amdgcn_sched_barrier(0);
+		}
+	}
 	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
 	cn.init(a, tid, NT);
 	if (tid < 6)
@@ -317,10 +402,6 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			wc_fl += (uint32_t)lane == j ? WF : 0u;
 		}
 	};
-	const uint32_t n = (uint32_t)a.n;
-	const uint32_t nt = (n + 63) / 64;
-	const uint32_t first = blockIdx.x * NW + wv;
-	const uint32_t step = gridDim.x * NW;
 	// xdp_stats_record_action (headers/xdp/xdp_stats_kern.h): per lane, the
 	// packets of each action in 10-bit fields of one word and their bytes
 	// in 21-bit fields of one double word -- a shift-add each per tile,
@@ -349,52 +430,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			st_fold();
 	};
 	uint32_t ndef = 0;
+	uint32_t vs_act = A_NONE, vs_gi = 0;   // (XFG_QT_VST) verdicts waiting for the next iteration's store
 
-	// windows + lengths of tile t (clamped to the last tile): CPP + 1 loads,
-	// always issued
-	// (the length width is a template parameter: one load of a fixed kind,
-	// so the compiler's wait counts stay exact across the loop)
-	constexpr uint32_t lsh = L16 ? 1u : 2u;
-	typedef typename std::conditional<L16, uint16_t, uint32_t>::type len_t;
-	const uint64_t lb = rfl64((uint64_t)(uintptr_t)a.lens);
-	auto ld_len = [](uint64_t p) {
-		const auto *q = reinterpret_cast<const __attribute__((address_space(1))) len_t *>(p);
-#if XFG_QT_NTLEN   /* (A/B: the lengths streamed like the windows) */
-		return __builtin_nontemporal_load(q);
-#else
-		return *q;
-#endif
-	};
-	// (a whole tile -- every one but a ragged last -- takes a uniform branch
-	// with no per-lane clamps: a scalar tile base and per-lane offsets that
-	// do not change from tile to tile; the same loads either way)
-	auto issue = [&](uint32_t t, u32x4 (&pre)[CPP], len_t &plen) {
-		t = t < nt ? t : nt - 1;
-		const uint32_t base = t * 64;
-		const uint32_t rem = n - base >= 64 ? 64u : n - base;
-		if (rem == 64) {
-			const uint8_t *tb = a.data + (uint64_t)base * (DENSE ? W : a.stride);
-#pragma unroll
-			for (int it = 0; it < CPP; it++) {
-				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
-				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
-							 : reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
-				pre[it] = __builtin_nontemporal_load(src);
-			}
-			plen = ld_len(lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
-		} else {
-#pragma unroll
-			for (int it = 0; it < CPP; it++) {
-				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
-				const uint32_t q = pk < rem ? pk : 0u;
-				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + (q * CPP + sub)
-							 : reinterpret_cast<const u32x4 *>(a.data + (uint64_t)(base + q) * a.stride + sub * 16);
-				pre[it] = __builtin_nontemporal_load(src);
-			}
-			const uint64_t la = lb + ((uint64_t)(base + ((uint32_t)lane < rem ? lane : 0u)) << lsh);
-			plen = ld_len(la);
-		}
-	};
 
 	auto pk3 = [](uint32_t act, uint32_t ps, uint32_t len) { return act | ps << 3 | len << 15; };
 	auto pk_act = [](uint32_t p) { return p & 7; };
@@ -449,9 +486,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// (wcf: this iteration moves completed hit-log chunks -- every other one:
 	// a ring of WR entries takes two iterations' hits with room to spare)
 	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen, RSt &rs, bool wcf) __attribute__((always_inline)) {
-		const uint32_t tP = first + k * step;
+		const uint32_t tP = tileOf(k);
 		const bool vP = tP < nt;
-		const bool vR = k >= LAG && tP - LAG * step < nt;
+		const uint32_t tR = k >= LAG ? tileOf(k - LAG) : nt;
+		const bool vR = tR < nt;
 		// everything but the newest iteration's loads (LAG 1: tile k+1's
 		// windows; LAG 2: also the last iteration's bucket loads; depth 3:
 		// also the windows issued the iteration before)
@@ -463,6 +501,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// rotates its zero-extension to the previous iteration's end, where
 		// it waits for the load -- and every older one -- early)
 		asm volatile("" : "+v"(curlen));
+		if constexpr (XFG_QT_VST) {   // (the last W's verdicts, their store acknowledged by the next wait)
+			if (vs_act <= A_PASS)
+				__builtin_nontemporal_store((uint8_t)vs_act, a.verdicts + vs_gi);
+			vs_act = A_NONE;
+		}
 
 		PMARK("R");
 		// ---- R: tile k-1's bucket -> CHECK_MAP (xdpfilt_prog.h:56-64)
@@ -471,7 +514,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// (both directions: W works on tile k-2, whose src lookup -- read
 		// last iteration for the packets whose dst lookup decided nothing --
 		// R2 resolves first; one directions: W works on tile k-1)
-		const bool vW = R2 ? (k >= LAG + 1 && tP - (LAG + 1) * step < nt) : vR;
+		const uint32_t tW = R2 ? (k >= LAG + 1 ? tileOf(k - LAG - 1) : nt) : tR;
+		const bool vW = tW < nt;
 		if constexpr (R2) {
 			PMARK("R2");
 			// lookup_verdict_ipv4 (xdpfilt_prog.h:121-134): the src key
@@ -595,9 +639,26 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 
 		PMARK("W");
 		// ---- W: verdicts, counters, stats, deferrals of tile k-1 (k-2)
+		auto stageW = [&]() __attribute__((always_inline)) {
 		if (vW) {
-			const uint32_t gi = (tP - (LAG + (R2 ? 1 : 0)) * step) * 64 + lane;
-			if (w_act <= A_PASS && !(dg & 8)) {
+			const uint32_t gi = tW * 64 + lane;
+			// (VGRP: a whole run's bytes gathered in LDS, stored as one
+			// dword a lane at its last tile; a deferred packet's byte is
+			// rewritten by the drain after the loop; a run past the batch's
+			// end: bytes as they come)
+			const uint32_t vj = tW % G;
+			const bool vrun = G > 1 && (tW - vj + G) * 64 <= n;
+			if (vrun) {
+				reinterpret_cast<uint8_t *>(s_vb)[wv * 256 + vj * 64 + lane] = (uint8_t)w_act;
+				if (vj == G - 1) {
+					__builtin_amdgcn_wave_barrier();
+					__builtin_nontemporal_store(s_vb[wv * 64 + lane],
+								    reinterpret_cast<uint32_t *>(a.verdicts + (tW - vj) * 64) + lane);
+				}
+			} else if constexpr (XFG_QT_VST) {
+				vs_act = (w_act <= A_PASS && !(dg & 8)) ? w_act : A_NONE;
+				vs_gi = gi;
+			} else if (w_act <= A_PASS && !(dg & 8)) {
 				__builtin_nontemporal_store((uint8_t)w_act, a.verdicts + gi);
 			}
 			count((dg & 1) ? CT_NONE : w_tag, (dg & 1) ? XFG_PORT_TAB : w_ps);
@@ -613,7 +674,22 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 		if (vW && logon && wcf)
 			wc_flush();
+		};
+		if constexpr (!XFG_QT_ORDER)
+			stageW();
 
+#if XFG_QT_PADV || XFG_QT_PADS
+		{   // (A/B: a fixed number of independent do-nothing instructions)
+			uint32_t pv = (uint32_t)lane, ps = k;
+#pragma unroll
+			for (int i = 0; i < XFG_QT_PADV; i++)
+				asm volatile("v_add_u32 %0, 1, %0" : "+v"(pv));
+#pragma unroll
+			for (int i = 0; i < XFG_QT_PADS; i++)
+				asm volatile("s_add_u32 %0, 1, %0" : "+s"(ps) :: "scc");
+			asm volatile("" ::"v"(pv), "s"(ps));
+		}
+#endif
 		PMARK("S");
 		// ---- S: tile k's windows into the rows, lengths clamped to the
 		// stride (rows past the batch's end hold a copy of the tile's first
@@ -698,6 +774,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			}
 		}
 		__builtin_amdgcn_sched_barrier(0);
+		if constexpr (XFG_QT_ORDER) {
+			stageW();
+			__builtin_amdgcn_sched_barrier(0);
+		}
 		PMARK("P");
 		// ---- P: parse tile k, hash its key, plan its fallback
 		uint32_t n6 = 0;   // (V6P) the tile's IPv6 lookups, at most 16
@@ -825,25 +905,14 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// (issued before the parse instead, the compiler's register
 		// reuse puts waits into R: not kept)
 		__builtin_amdgcn_sched_barrier(0);
-		issue(tP + D * step, cur, curlen);
+		issue(tileOf(k + D), cur, curlen);
 		__builtin_amdgcn_sched_barrier(0);
 	};
 
-	u32x4 preA[CPP], preB[CPP], preC[D == 3 ? CPP : 1];
-	len_t lenA = 0, lenB = 0, lenC = 0;
-	if (nt) {
-		issue(first, preA, lenA);
-		__builtin_amdgcn_sched_barrier(0);
-		issue(first + step, preB, lenB);
-		__builtin_amdgcn_sched_barrier(0);
-		if constexpr (D == 3) {
-			issue(first + 2 * step, preC, lenC);
-			__builtin_amdgcn_sched_barrier(0);
-		}
-	}
 	// (one more with both directions: the last tile's src lookup resolves
 	// an iteration after its dst lookup)
-	const uint32_t iters = first < nt ? (nt - 1 - first) / step + 1 + LAG + (R2 ? 1 : 0) : 0u;
+	const uint32_t nrun = (nt + G - 1) / G;
+	const uint32_t iters = first < nrun ? ((nrun - 1 - first) / step + 1) * G + LAG + (R2 ? 1 : 0) : 0u;
 	// iteration k uses window buffer k % D and state set k % LAG: the loop
 	// body is U = lcm(D, LAG) iterations
 	constexpr uint32_t U = D == 3 ? 3 * LAG : 2;
@@ -894,6 +963,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		}
 	}
 
+	if constexpr (XFG_QT_VST)
+		if (vs_act <= A_PASS)
+			__builtin_nontemporal_store((uint8_t)vs_act, a.verdicts + vs_gi);
+	if constexpr (G > 1)   // (the runs' verdict dwords before the drain rewrites bytes in them)
+		__builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 	if (dg & 2048)
 		ndef = 0;
 	// the deferred packets: the whole reference walk over the canonical
