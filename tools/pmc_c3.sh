@@ -1,4 +1,4 @@
-# PMC passes of the product QT kernel on C3 at 2^26 (explore.py through the
+# PMC passes of the product QT kernel on C3 at 2^26 (TAG names the files) (explore.py through the
 # product library), one rocprofv3 --pmc run per counter group.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONUNBUFFERED=1
 export XFG_LIB=$GRAFT_REPO_ROOT/xdp-tools_amd/lib/libxdpfilter_gpu.so KNAME=pipeq

@@ -79,6 +79,9 @@
 #ifndef XFG_QT_VGRP      /* 1: a wave's tiles in runs of 4 consecutive tiles, verdicts stored 256 B at once */
 #define XFG_QT_VGRP 0
 #endif
+#ifndef XFG_QT_CNT2      /* 1: the hit's ring atomics without exec masks (a word per lane past the rings) */
+#define XFG_QT_CNT2 1
+#endif
 #ifndef XFG_QT_PADV      /* (A/B only: extra VALU / SALU instructions per tile, to price one) */
 #define XFG_QT_PADV 0
 #endif
@@ -163,8 +166,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// gives their places back.  A hit that finds the ring full (a hot key)
 	// is summed in the LDS counter cache instead (QT tag), as is a chunk
 	// that would overrun the slice.  No per-wave log, no workgroup-end sort.
-	constexpr uint32_t PPW = XFG_LOG_PARTS / NW;   // partitions a wave owns (ownp)
-	static_assert(PPW * NW == XFG_LOG_PARTS && PPW <= 64, "partition ownership");
+	// partitions a wave owns (ownp): wave wv the consecutive run
+	// [wv * 256 / NW, (wv + 1) * 256 / NW) -- PPW of them, or one fewer when
+	// NW does not divide 256
+	constexpr uint32_t PPW = (XFG_LOG_PARTS + NW - 1) / NW;
+	static_assert(PPW <= 64 && (XFG_QT_OWNC || PPW * NW == XFG_LOG_PARTS), "partition ownership");
 	// (WIDE: an index past 2^20 buckets -- local indices past 16 bits -- logs
 	// u32 entries, a ring of the same bytes: half the entries; with 64-byte
 	// windows a flush chunk is still a line)
@@ -173,16 +179,25 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr uint32_t WF = W <= 64 ? XFG_QT_WC_F / (WIDE ? 2 : 1) : WR / 2;   // flush chunk
 	static_assert((WR & (WR - 1)) == 0 && WF <= 64, "ring: a power of two");
 	__shared__ __attribute__((aligned(16))) uint32_t win[NW * 64 * ROWDW];
-	__shared__ ring_t s_ring[XFG_LOG_PARTS * WR];
-	__shared__ uint32_t s_res[XFG_LOG_PARTS];
-	__shared__ __attribute__((aligned(8))) uint32_t s_hd[2 * XFG_LOG_PARTS];
+	// (CNT2: 64 words past the partitions, one a lane, take the atomics of
+	// the lanes without a logged hit -- or a port hit -- so that the whole
+	// wave runs them with no exec mask)
+	constexpr uint32_t XL = XFG_QT_CNT2 ? 64u : 0u;
+	__shared__ ring_t s_ring[XFG_LOG_PARTS * WR + XL];
+	__shared__ uint32_t s_res[XFG_LOG_PARTS + XL];
+	__shared__ __attribute__((aligned(8))) uint32_t s_hd[2 * (XFG_LOG_PARTS + XL)];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
-	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB : 1];
+	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB + XL : 1];
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
 	__shared__ uint32_t s_lh[XFG_LOG_PARTS];
 	__shared__ unsigned long long s_stats[6];
 	__shared__ uint32_t s6b[V6P ? NW * (V6B ? 32 : 16) : 1];   // (V6P) a tile's IPv6 home buckets, by rank (V6B: + src)
-	__shared__ u32x4 s6l[V6P ? NW * 64 : 1];      // (V6P) their lines, four lanes each
+	// (their lines, four lanes each; an A/B build with more than 8 waves has
+	// no room for them: its IPv6-lookup variants trap rather than launch)
+	constexpr bool V6ROOM = NW <= 8;
+	__shared__ u32x4 s6l[V6P && V6ROOM ? NW * 64 : 1];
+	if constexpr (V6P && !V6ROOM)
+		__builtin_trap();
 	constexpr uint32_t G = XFG_QT_VGRP ? 4u : 1u;   // tiles per run (VGRP)
 	__shared__ uint32_t s_vb[G > 1 ? NW * 64 : 1];   // (VGRP) a run's verdict bytes, per wave
 	extern __shared__ uint32_t s_dyn[];
@@ -296,11 +311,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	const bool ptab = PORTS && a.port_count && a.port_tab;
 	const uint32_t pdisp = rfl(a.port_tab_disp), gb3 = rfl(a.gbase[3]);
 	if constexpr (PORTS)
-		for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
+		for (int i = tid; i < (int)(XFG_PORT_TAB + XL); i += NT)
 			s_pcnt[i] = 0;
 	for (int i = tid; i < (int)XFG_LOG_PARTS; i += NT)
 		s_lh[i] = 0;
-	for (int i = tid; i < (int)XFG_LOG_PARTS; i += NT) {
+	for (int i = tid; i < (int)(XFG_LOG_PARTS + XL); i += NT) {
 		s_res[i] = 0;
 		s_hd[2 * i] = 0;
 		s_hd[2 * i + 1] = 0;
@@ -308,7 +323,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// this lane's partition (lanes below PPW), the entries it has moved out
 	// (OWNC: wave wv owns partitions wv * PPW .. + PPW - 1, so its lanes' head /
 	// done words are consecutive: one conflict-free 8-byte LDS read)
-	auto ownp = [&](uint32_t j) { return XFG_QT_OWNC ? (uint32_t)wv * PPW + j : j * NW + (uint32_t)wv; };
+	const uint32_t pbase = (uint32_t)wv * XFG_LOG_PARTS / NW;
+	const uint32_t pcnt = ((uint32_t)wv + 1) * XFG_LOG_PARTS / NW - pbase;   // (uniform: PPW or PPW - 1)
+	auto ownp = [&](uint32_t j) { return XFG_QT_OWNC ? pbase + j : j * NW + (uint32_t)wv; };
 	const uint32_t wc_p = ownp((uint32_t)lane);
 	uint32_t wc_fl = 0;
 	const uint64_t wc_slice0 = (uint64_t)(blockIdx.x + a.pslice0) * a.pcap;
@@ -329,6 +346,38 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		const bool ps = pslot < XFG_PORT_TAB;
 		const bool dc = !q & (tag < a.dcnt);
 		const uint32_t qs = tag & ~QTAG;
+		if constexpr (XFG_QT_CNT2) {
+			if (!(dg & 4096)) {
+				// the ring's protocol (below) run by every lane: a lane
+				// without a logged hit reserves, takes a ticket, writes and
+				// counts done on its own words past the partitions
+				const bool ql = q & logon;
+				const uint32_t dm = XFG_LOG_PARTS + (uint32_t)lane;
+				const uint32_t p = ql ? log_part(qs) : dm;
+				const uint32_t r = atomicAdd(&s_res[p], 1u);
+				const bool ok = ql & (r < WR);
+				const uint32_t ph = ok ? p : dm;
+				const uint32_t t = atomicAdd(&s_hd[2 * ph], 1u);
+				s_ring[ok ? p * WR + (t & (WR - 1)) : XFG_LOG_PARTS * WR + (uint32_t)lane] =
+					(ring_t)log_local(qs);
+				atomicAdd(&s_hd[2 * ph + 1], 1u);
+				if constexpr (PORTS)
+					atomicAdd(&s_pcnt[ps ? pslot : XFG_PORT_TAB + (uint32_t)lane], 1u);
+				// rare: a full ring (or no log), counter identities other
+				// than QT slots and ports
+				const bool slow = (q & !ok) | (!q & !ps & (tag != CT_NONE));
+				if (__ballot(slow)) {
+					if (ql & !ok)
+						atomicSub(&s_res[p], 1u);
+					if ((q & !ok) && !cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
+						atomicAdd(a.qt_hits + qs, 1ull);
+					if (dc & !ps)
+						atomicAdd(&cn.dcnt[tag], 1u);
+					cn.bump(a, pick(q | dc | ps, CT_NONE, tag), lane);
+				}
+				return;
+			}
+		}
 		if (dg & 4096) {   // (diagnostics: a memory-side atomic per hit into scratch)
 			if (q)
 				atomicAdd(reinterpret_cast<uint32_t *>(a.pbuf) + qs, 1u);
@@ -386,12 +435,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// head and done of the partition in ONE 8-byte read (a snapshot):
 		// done == head means every ticket taken has been written
 		uint32_t hd0 = 0, hd1 = 0;
-		if ((uint32_t)lane < PPW) {
+		if ((uint32_t)lane < pcnt) {
 			const uint64_t v = *reinterpret_cast<const uint64_t *>(&s_hd[2 * wc_p]);
 			hd0 = (uint32_t)v;
 			hd1 = (uint32_t)(v >> 32);
 		}
-		unsigned long long fm = __ballot(((uint32_t)lane < PPW) & (hd0 == hd1) & (hd1 - wc_fl >= WF));
+		unsigned long long fm = __ballot(((uint32_t)lane < pcnt) & (hd0 == hd1) & (hd1 - wc_fl >= WF));
 		while (fm) {
 			const uint32_t j = (uint32_t)__ffsll((long long)fm) - 1;
 			fm &= fm - 1;
@@ -1008,17 +1057,17 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// wave's partitions, and the slices' fills for the count kernel; a
 	// position past a slice goes to the counter cache, flushed below
 	if (a.pbuf && !(dg & 16)) {
-		const uint32_t hd = (uint32_t)lane < PPW ? s_hd[2 * wc_p] : 0u;
+		const uint32_t hd = (uint32_t)lane < pcnt ? s_hd[2 * wc_p] : 0u;
 		// (every position within its slice -- the usual case: two rings
 		// per instruction, 8 bytes a lane, one LDS read and one store each
 		// for the lanes whose entries are consecutive tickets; a ring holds
 		// tickets [fl, h) at slots t & (WR - 1), so slot s carries ticket
 		// fl + ((s - fl) & (WR - 1)), 8-byte aligned in the slice)
 		constexpr uint32_t EPL = 8 / sizeof(ring_t);
-		if (WR * sizeof(ring_t) == 256 && __ballot(((uint32_t)lane < PPW) & (hd > a.pcap)) == 0) {
+		if (WR * sizeof(ring_t) == 256 && __ballot(((uint32_t)lane < pcnt) & (hd > a.pcap)) == 0) {
 			const uint32_t half = (uint32_t)lane >> 5, s0 = ((uint32_t)lane & 31) * EPL;
 #pragma unroll 4
-			for (uint32_t j = 0; j < PPW; j += 2) {
+			for (uint32_t j = 0; j < pcnt; j += 2) {
 				const uint32_t fl = half ? __builtin_amdgcn_readlane(wc_fl, j + 1) : __builtin_amdgcn_readlane(wc_fl, j);
 				const uint32_t h = half ? __builtin_amdgcn_readlane(hd, j + 1) : __builtin_amdgcn_readlane(hd, j);
 				const uint32_t p = ownp(j + half);
@@ -1038,13 +1087,13 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				}
 			}
 		} else {
-			for (uint32_t j = 0; j < PPW; j++) {
+			for (uint32_t j = 0; j < pcnt; j++) {
 				const uint32_t fl = __builtin_amdgcn_readlane(wc_fl, j);
 				const uint32_t h = __builtin_amdgcn_readlane(hd, j);
 				wc_move(j, fl, h - fl);
 			}
 		}
-		if ((uint32_t)lane < PPW)
+		if ((uint32_t)lane < pcnt)
 			gst32(a.pfill + (uint64_t)wc_p * a.pslices + a.pslice0 + blockIdx.x, hd);
 	}
 	__syncthreads();
