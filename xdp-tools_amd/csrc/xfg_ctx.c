@@ -82,7 +82,7 @@ struct xfg_dev {
 	 * 5 pipelined IPv4-key mode over the quotient index]
 	 * [window 64, 128][dynamic LDS: none, direct counters, port nibble map,
 	 * both] */
-	int occ[6][2][4];
+	int occ[6][2][8];   /* [..][dynamic LDS: + bit 2, the Bloom words (bl_lds)] */
 	/* quotient index of the IPv4 map (kind 5 kernel), uploaded from
 	 * ctx->qt when qt_gen falls behind ctx->qt_gen; params read at launch
 	 * under d->lock */
@@ -460,10 +460,11 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 
 	for (int k = 0; k < 6; k++)
 		for (int w = 0; w < 2; w++)
-			for (int c = 0; c < 4; c++)
+			for (int c = 0; c < 8; c++)
 				d->occ[k][w][c] = xfg_classify_occupancy(
 					ctx->prog_features, k, w ? 128 : 64,
-					(c & 1 ? XFG_DCNT_MAX * 4 : 0) + (c & 2 ? XFG_PORT_NIB_WORDS * 4 : 0));
+					(c & 1 ? XFG_DCNT_MAX * 4 : 0) + (c & 2 ? XFG_PORT_NIB_WORDS * 4 : 0) +
+					(c & 4 ? XFG_BLOOM_LDS_MAX * 4 : 0));
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -1570,7 +1571,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	int qt_nolog = 0;
 	if (a.qt) {
 		const int k5 = 5, wi5 = a.window > 64;
-		const int pc = d->occ[k5][wi5][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
+		const int pc = d->occ[k5][wi5][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) | (a.bl_lds ? 4 : 0)];
 		const uint64_t pw = (uint64_t)xfg_classify_threads(k5, a.window);
 		uint64_t g5 = (uint64_t)d->ncu * (pc > 0 ? pc : 1), need5 = (a.n + pw - 1) / pw;
 		if (g5 > need5)
@@ -1588,6 +1589,26 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	if (!a.qt && a.v6d) {   /* (the IPv6 keys need the general kernel then) */
 		a.km = 0;
 		a.v6d = 0;
+	}
+	/* the generic pipelined kernel: small maps' Bloom filters staged in LDS */
+	a.bl_lds = 0;
+	if (a.pipe && !a.km) {
+		const struct xfg_tdesc *tt[3] = { &a.t4, &a.te, &a.t6 };
+		uint32_t tot = 0;
+		for (int i = 0; i < 3; i++) {
+			a.bl_off[i] = ~0u;
+			if (tt[i]->count && tt[i]->bloom_words) {
+				a.bl_off[i] = tot;
+				tot += tt[i]->bloom_words;
+			}
+		}
+		if (tot <= XFG_BLOOM_LDS_MAX)
+			a.bl_lds = tot;
+#ifdef XFG_DIAG
+		const char *bl = getenv("XFG_BLOOM_LDS");   /* "off": the words from memory */
+		if (bl && !strcmp(bl, "off"))
+			a.bl_lds = 0;
+#endif
 	}
 	const int kind = a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
 	if (a.qt) {   /* the index in stream order at this launch */
@@ -1611,7 +1632,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			goto out;
 		a.qt_hits = d->qt_hits;
 	}
-	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0)];
+	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) | (a.bl_lds ? 4 : 0)];
 #ifdef XFG_DIAG
 	const char *g = getenv("XFG_GRID_PER_CU");
 	if (g && *g)

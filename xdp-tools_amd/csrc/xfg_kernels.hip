@@ -1535,7 +1535,7 @@ void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 template <uint32_t FEAT>
 hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 {
-	const size_t dl = (size_t)a.dcnt * 4 +
+	const size_t dl = (size_t)a.dcnt * 4 + (size_t)a.bl_lds * 4 +
 			  (a.port_nib && !a.port_tab && a.port_count ? XFG_PORT_NIB_WORDS * 4 : 0);
 	if (a.pipe) {
 		bool done = false;

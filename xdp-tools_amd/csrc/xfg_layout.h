@@ -84,6 +84,7 @@
 #define XFG_PORT_NIB_WORDS 8192u  /* more: every port's 4 flag bits, 32 KiB of LDS */
 
 #define XFG_BLOOM_K       4u
+#define XFG_BLOOM_LDS_MAX 4096u   /* Bloom words a generic pipelined workgroup stages in LDS (16 KiB) */
 
 #define XFG_QT_SLOTS      16u     /* entries per 32-byte QT bucket */
 #define XFG_QT_BUCKET     32u
@@ -163,6 +164,13 @@ struct xfg_kargs {
 	/* Direct LDS counters: identities below dcnt (all hash maps, gbase[3],
 	 * or the IPv4 map, gbase[1]) are summed per workgroup in LDS; 0 = off */
 	uint32_t dcnt;
+	/* The generic pipelined kernel's Bloom words in LDS, past the direct
+	 * counters: bl_lds words in all, bl_off[i] the first of table i (t4,
+	 * te, t6; ~0u: not staged) -- when every live map's filter fits in
+	 * XFG_BLOOM_LDS_MAX words (C1's 10,000-entry Ethernet map: 3,750); 0 =
+	 * the words read from memory */
+	uint32_t bl_lds;
+	uint32_t bl_off[3];
 	/* Hit log of the pipelined kernels (tlog NULL = no log): per-wave
 	 * regions of defer_cap counter identities; partition-major buffer of
 	 * XFG_LOG_PARTS x pslices slices of pcap entries, slice (p, b) owned by

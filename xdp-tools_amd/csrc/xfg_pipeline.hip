@@ -130,7 +130,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x)
 template <int KM>
 struct KTabs {
 	static constexpr int NK = KM == 1 ? 1 : 3;   // tables held (KM 1: IPv4 only)
-	uint32_t nb[NK], md[NK], ns[NK], zp[NK], bw[NK], gb[NK];
+	uint32_t nb[NK], md[NK], ns[NK], zp[NK], bw[NK], gb[NK], blo[NK];
 	uint64_t bk[NK], bl[NK];
 	__device__ __forceinline__ void load(const xfg_kargs &a)
 	{
@@ -144,6 +144,7 @@ struct KTabs {
 			zp[i] = rfl(t[i]->zero_present);
 			bw[i] = rfl(t[i]->bloom_words);
 			gb[i] = rfl(g[i]);
+			blo[i] = rfl(a.bl_off[i]);
 			bk[i] = rfl64((uint64_t)(uintptr_t)t[i]->buckets);
 			bl[i] = rfl64((uint64_t)(uintptr_t)t[i]->bloom);
 		}
@@ -421,6 +422,21 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 	if (tid < 6)
 		s_stats[tid] = 0;
 	const uint32_t *s_ports = stage_ports<FEAT>(a, s_tab, s_dyn, tid, NT);
+	// (bl_lds: the live maps' Bloom filters copied into LDS, past the direct
+	// counters -- the probes of small rule sets then read no memory: C1's
+	// filter, 15 KB of random words, cost a random line per probe)
+	uint32_t *const s_bl = dcnt_base(a, s_dyn) + a.dcnt;
+	const bool bll = a.bl_lds != 0;
+	if (bll) {
+#pragma unroll
+		for (int i = 0; i < KTabs<KM>::NK; i++) {
+			if (T.blo[i] == ~0u)
+				continue;
+			const uint32_t *src = reinterpret_cast<const uint32_t *>(T.bl[i]);
+			for (uint32_t w = tid; w < T.bw[i]; w += NT)
+				s_bl[T.blo[i] + w] = src[w];
+		}
+	}
 	__syncthreads();
 
 	uint32_t *const rows = win + wv * 64 * ROWDW;
@@ -652,8 +668,9 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 				q_w[i] = ~0u;
 				if ((uint32_t)i < q_nk && !kd_zero(q_kd[i])) {
 					const uint32_t kind = KM == 1 ? K_V4 : kd_kind(q_kd[i]);
-					q_w[i] = gload32(TSEL(T, kind, bl) +
-							 4ull * xfg_bloom_word(q_kh[i], TSEL(T, kind, bw)));
+					const uint32_t bwi = xfg_bloom_word(q_kh[i], TSEL(T, kind, bw));
+					q_w[i] = bll ? s_bl[TSEL(T, kind, blo) + bwi]
+						     : gload32(TSEL(T, kind, bl) + 4ull * bwi);
 				}
 			}
 		}
