@@ -226,7 +226,8 @@ def main():
             f.classify_host(hdata, hlens, stride=stride)
         hs = (time.perf_counter() - t0) / reps
         # the same batch registered once (xfg_host_register, as a long-lived
-        # capture ring or UMEM would be): DMA where it lies, no staging copy
+        # capture ring or UMEM would be): the kernels read its mapped pages
+        # in place (zero copy), no staging
         f.host_register(hdata)
         f.classify_host(hdata, hlens, stride=stride)
         t0 = time.perf_counter()
@@ -240,7 +241,7 @@ def main():
                      "registered_GBps_h2d": round(hdata.nbytes / hr / 1e9, 1),
                      "note": "host-resident batch incl. H2D frames+lens and D2H verdicts "
                              "(xfg_classify_host: pinned staging copy by the device's pool; "
-                             "registered: DMA from the caller's pages)"}
+                             "registered: the kernels read the caller's mapped pages in place)"}
         del hdata
 
     # ---- CPU baseline (rank 0, N=1 only)

@@ -221,7 +221,8 @@ int xfg_classify_descs(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *batch
  * / D2H over chunks; a frame whose program reads past its window is sent
  * again whole and classified from it, so verdicts, counters and stats are
  * exactly those of a whole-frame run.  A fixed stride of at most 128 bytes
- * is staged slot for slot.  Concurrent calls on different devices run in
+ * is staged slot for slot; a batch in a registered buffer
+ * (xfg_host_register) is read in place instead.  Concurrent calls on different devices run in
  * parallel; staging memory per device is fixed (about 70 MB pinned).
  * Replaces the per-packet program run of the attach path
  * (xdp-filter/xdpfilt_prog.h:214-310 over frames the kernel hands it).
@@ -231,11 +232,14 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
 
 /*
  * Register a long-lived host buffer (a capture ring, an AF_XDP UMEM) for
- * direct DMA: a host batch whose fixed-stride slots (stride <= 128) lie
- * inside a registered buffer is copied to the device where it lies, with
- * no staging copy.  Pins the pages (hipHostRegister) until
- * xfg_host_unregister() or xfg_close().  At most 16 buffers per context;
- * -EEXIST if it overlaps a registered one.
+ * zero-copy reads: a host batch whose fixed-stride slots (stride a multiple
+ * of 16) lie inside a registered buffer, or an AF_XDP batch
+ * (xfg_classify_xsk_host) whose UMEM does, is read by the kernels where it
+ * lies through the buffer's device mapping -- only the bytes the programs
+ * load cross PCIe, and no frame is staged.  Pins and maps the pages
+ * (hipHostRegister, portable + mapped) until xfg_host_unregister() or
+ * xfg_close().  At most 16 buffers per context; -EEXIST if it overlaps a
+ * registered one.
  */
 int xfg_host_register(xfg_ctx *ctx, void *p, size_t bytes);
 int xfg_host_unregister(xfg_ctx *ctx, void *p);
@@ -250,8 +254,8 @@ int xfg_host_unregister(xfg_ctx *ctx, void *p);
  * (addr >> 48) (xsk_umem__add_offset_to_addr(), headers/xdp/xsk.h:173-186;
  * unaligned-chunk mode).  mask = ring entries - 1 (a power of two), or
  * 0xffffffff for a plain array; count <= entries.  Classified as
- * xfg_classify_host does (header windows, exact whole-frame fallback);
- * -EINVAL if a frame lies outside the UMEM.  The caller releases the ring
+ * xfg_classify_host does (header windows, exact whole-frame fallback; a
+ * registered UMEM read in place); -EINVAL if a frame lies outside the UMEM.  The caller releases the ring
  * entries after the call returns.
  */
 int xfg_classify_xsk_host(xfg_ctx *ctx, int dev, const struct xfg_desc_batch *batch,

@@ -355,11 +355,13 @@ def test_classify_host_header_windows_exact(G, layout):
     f.close()
 
 
-def test_classify_xsk_host_ring_wrap_unaligned(G):
+@pytest.mark.parametrize("registered", [False, True])
+def test_classify_xsk_host_ring_wrap_unaligned(G, registered):
     """The host-memory AF_XDP consumer (xfg_classify_xsk_host): a UMEM of
     4 KiB chunks in host memory, frames at aligned and unaligned-chunk
     addresses (offset in bits 48..63, headers/xdp/xsk.h:173-186), an RX ring
-    view that wraps; long-header frames take the whole-frame fallback."""
+    view that wraps; long-header frames take the whole-frame fallback, or,
+    with the UMEM registered, every frame is read in place (zero copy)."""
     rules, pool = X.random_rules(111, n4=120, n6=60, ne=20, nports=30)
     fd, fl = X.gen_fuzz(29, 20000, 160, rules, pool)
     frames = P.frames_of(fd, fl, stride=160) + _long_header_frames(rules, 1500, 9)
@@ -383,6 +385,8 @@ def test_classify_xsk_host_ring_wrap_unaligned(G):
     descs[idx, 1] = lens.astype(np.uint64)
     f = G.Filter(feats, ndev=1)
     f.load_rules(rules)
+    if registered:
+        f.host_register(umem)
     v = f.classify_xsk_host(umem, descs, n, first=first, mask=ring - 1)
     np.testing.assert_array_equal(v, ov)
     np.testing.assert_array_equal(f.stats(), ost)
@@ -396,6 +400,8 @@ def test_classify_xsk_host_ring_wrap_unaligned(G):
         f.classify_xsk_host(umem, bad, n, first=first, mask=ring - 1)
     with pytest.raises(OSError):      # a ring mask must be 2^k - 1
         f.classify_xsk_host(umem, descs, n, first=first, mask=1000)
+    if registered:
+        f.host_unregister(umem)
     f.close()
 
 
@@ -482,9 +488,9 @@ def test_cli_run_capture_with_one_huge_frame(G, cli, tmp_path):
 
 
 def test_classify_host_registered_buffer(G):
-    """xfg_host_register: a registered 64-byte-stride batch is copied to the
-    device where it lies (no staging copy); same verdicts, counters and
-    stats; overlapping registration and unknown unregister are refused."""
+    """xfg_host_register: a registered 64-byte-stride batch is read by the
+    kernels where it lies (zero copy, no staging); same verdicts, counters
+    and stats; overlapping registration and unknown unregister are refused."""
     n = (1 << 19) + 5
     v4 = X.rand_keys(3, 20000, 4)
     ports = np.array([53, 80], np.uint16)
@@ -508,4 +514,32 @@ def test_classify_host_registered_buffer(G):
     f.host_unregister(data)
     with pytest.raises(OSError):
         f.host_unregister(data)
+    f.close()
+
+
+@pytest.mark.parametrize("stride,first", [(1536, 0), (1536, 777), (128, 4099), (168, 0)])
+def test_classify_host_registered_slices(G, stride, first):
+    """Registered batches the zero-copy path reads in place: large slots
+    (whole 1514-byte frames, walked past the window by the IPv6 extension
+    headers), a batch starting inside the registered buffer (the device
+    address offset), and a stride the kernels' 16-byte loads cannot take in
+    place (168: the staging path) -- all equal to the restatement."""
+    n = 40000 if stride > 128 else 300000
+    rules, pool = X.random_rules(71 + stride, n4=300, n6=100, ne=20, nports=40)
+    data, lens = X.gen_fuzz(5 + first, n + first, stride, rules, pool)
+    feats = X.VARIANT_FEATURES["xdpfilt_alw_all"]
+    sub = data[first * stride:]
+    slens = lens[first:].astype(np.uint32)
+    slens[-1] = 65000                     # past its slot: capped at the stride
+    ov, _, ost = X.run_oracle(feats, sub, np.minimum(slens, stride), rules, stride=stride,
+                              nthreads=8)
+    f = G.Filter(feats, ndev=1)
+    f.load_rules(rules)
+    f.host_register(data)
+    try:
+        v = f.classify_host(sub, slens, stride=stride)
+    finally:
+        f.host_unregister(data)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(f.stats(), ost)
     f.close()

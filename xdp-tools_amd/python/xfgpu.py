@@ -412,7 +412,8 @@ class Filter:
                "classify_descs")
 
     def host_register(self, arr: np.ndarray):
-        """Pin a long-lived host array for direct DMA (xfg_host_register)."""
+        """Pin and map a long-lived host array: the kernels read batches in it
+        in place (xfg_host_register, zero copy)."""
         _check(lib.xfg_host_register(self.ctx, arr.ctypes.data, arr.nbytes), "host_register")
 
     def host_unregister(self, arr: np.ndarray):
