@@ -42,6 +42,7 @@ KERNEL_OF_PATH = {
     1: "xfg_pipeline_kernel (generic pipelined)",
     2: "xfg_pipe4_kernel (IPv4-key pipelined)",
     5: "xfg_pipeq_kernel (IPv4-key pipelined over the quotient index)",
+    6: "xfg_pipee_kernel (Ethernet-key, the map as an LDS key table)",
 }
 # rocprofv3 --pmc summaries of the bench's own workload (tools/pmc.sh,
 # tools/pmc_summary.py): per launch path, the file and the batch it was taken at

@@ -72,7 +72,7 @@ def check(G, variant, rules, data, lens, stride, host=False, path=None, **caps):
 def test_c1_alw_eth_8_mac_rules(G):
     rules = X.c1_rules()
     data, lens = X.gen_c1(1, 1 << 22)
-    ov = check(G, "xdpfilt_alw_eth", rules, data, lens, 64)
+    ov = check(G, "xdpfilt_alw_eth", rules, data, lens, 64, path=6)
     # a quarter of the frames carry a ruled MAC where its rule tests it: DROP
     # under allow mode (xdpfilt_prog.h:187-196)
     assert abs(int((ov == 1).sum()) - (1 << 20)) < (1 << 14)

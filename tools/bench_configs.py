@@ -55,6 +55,12 @@ def run_c1(args):
     ms = f.classify_timed(d_data.ptr, d_lens.ptr, n, 64, d_verd.ptr, args.iters)
     path = f.last_path()
     f.close()
+    if args.no_cpu:
+        print(json.dumps({"config": "c1", "packets": n, "kernel_path": path,
+                          "kernel_ms": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+                          "roofline": {"frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}),
+              flush=True)
+        return
     # the CPU restatement on the same batch: 1 thread and every usable core
     # (a bounded sample: whole passes until ~4 s each)
     feats = X.VARIANT_FEATURES["xdpfilt_alw_eth"]
@@ -172,6 +178,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["c2", "c4", "c5", "c3sd"])
     ap.add_argument("--log2-packets", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true", help="c1: the GPU leg only")
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     for c in a.configs:

@@ -79,10 +79,17 @@ struct xfg_dev {
 	int port_tab_ok, port_tab_dirty;
 	/* resident classify workgroups per CU: [kernel: 0 general, 1 pipelined,
 	 * 2 pipelined IPv4-key mode, 3 split lookup pass, 4 split parse pass,
-	 * 5 pipelined IPv4-key mode over the quotient index]
+	 * 5 pipelined IPv4-key mode over the quotient index, 6 Ethernet-key]
 	 * [window 64, 128][dynamic LDS: none, direct counters, port nibble map,
 	 * both] */
-	int occ[6][2][8];   /* [..][dynamic LDS: + bit 2, the Bloom words (bl_lds)] */
+	int occ[7][2][8];   /* [..][dynamic LDS: + bit 2, the Bloom words (bl_lds),
+			     * kind 6: the LDS key table] */
+	/* the Ethernet-key kernel's key table (kind 6), uploaded from ctx->ek
+	 * when ek_gen falls behind ctx->ek_gen; params read at launch under
+	 * d->lock */
+	uint32_t *ek_img;
+	uint64_t ek_img_bytes;
+	uint32_t ek_gen, ek_slots, ek_disp;
 	/* quotient index of the IPv4 map (kind 5 kernel), uploaded from
 	 * ctx->qt when qt_gen falls behind ctx->qt_gen; params read at launch
 	 * under d->lock */
@@ -157,6 +164,15 @@ struct xfg_ctx {
 	struct xfg_qt qt;
 	int qt_dirty;
 	uint32_t qt_gen;
+	/* the Ethernet map as the Ethernet-key kernel's LDS key table
+	 * (xfg_kargs.ek): rebuilt when an Ethernet flag byte or key changed
+	 * (ek_edits moved past ek_built); ek_ok: it can serve (few keys, the
+	 * same flags on every device) */
+	uint32_t ek_host[XFG_EK_SLOTS_MAX * 4];
+	uint32_t ek_slots, ek_disp;
+	uint32_t ek_edits, ek_seen;   /* Ethernet map edits; those the table holds */
+	uint32_t ek_gen;              /* tables built (0: none yet) */
+	int ek_ok;
 	uint32_t qt_min_keys;
 	uint32_t window;                /* header window above a 64-byte stride: 64 or 128 */
 	uint32_t port_flag_cnt[8];
@@ -368,6 +384,7 @@ static void dev_free(struct xfg_dev *d)
 	hipFree(d->sink);
 	hipFree(d->port_tab);
 	hipFree(d->qt_img);
+	hipFree(d->ek_img);
 	hipFree(d->qt_trans);
 	hipFree(d->qt_hits);
 	free(d->port_flags_h);
@@ -458,13 +475,13 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
 
-	for (int k = 0; k < 6; k++)
+	for (int k = 0; k < 7; k++)
 		for (int w = 0; w < 2; w++)
 			for (int c = 0; c < 8; c++)
 				d->occ[k][w][c] = xfg_classify_occupancy(
 					ctx->prog_features, k, w ? 128 : 64,
 					(c & 1 ? XFG_DCNT_MAX * 4 : 0) + (c & 2 ? XFG_PORT_NIB_WORDS * 4 : 0) +
-					(c & 4 ? XFG_BLOOM_LDS_MAX * 4 : 0));
+					(c & 4 ? (k == 6 ? XFG_EK_SLOTS_MAX * 16 : XFG_BLOOM_LDS_MAX * 4) : 0));
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -721,6 +738,8 @@ static uint8_t flags_note(xfg_ctx *ctx, int mi, uint64_t slot, uint8_t any, uint
 {
 	const uint8_t f = any | (any != all ? 0x80 : 0), old = ctx->flag_or[mi][slot];
 	census(ctx->flag_cnt[mi], old, f);
+	if (mi == 2)   /* (every key insert and delete passes here) */
+		ctx->ek_edits++;
 	ctx->flag_or[mi][slot] = f;
 	if (mi == 0 && old != f && !patch)
 		ctx->qt_dirty = 1;
@@ -1384,6 +1403,60 @@ static int qt_refresh(xfg_ctx *ctx, struct xfg_dev *d, uint32_t live)
 	return err;
 }
 
+/* The Ethernet map as the Ethernet-key kernel's key table (ctx->lock held):
+ * rebuilt on the host after an edit, then uploaded to @d when its copy is
+ * older.  A key at home xfg_hash_eth & (slots - 1), linear probing; slots
+ * at least twice the keys.  ek_ok 0 (the generic kernel instead): more than
+ * XFG_EK_MAX_KEYS keys, or a flag byte that differs between devices. */
+static int ek_refresh(xfg_ctx *ctx, struct xfg_dev *d)
+{
+	int err = 0;
+	const struct xfg_table *t = &ctx->t[2];
+	if (!ctx->ek_gen || ctx->ek_seen != ctx->ek_edits) {
+		ctx->ek_seen = ctx->ek_edits;
+		if (!++ctx->ek_gen)
+			ctx->ek_gen = 1;
+		ctx->ek_ok = t->count <= XFG_EK_MAX_KEYS && !ctx->flag_cnt[2][7];
+		if (!ctx->ek_ok)
+			return 0;
+		uint32_t sl = 64;
+		while (sl < 2 * t->count)
+			sl *= 2;
+		memset(ctx->ek_host, 0, (size_t)sl * 16);
+		ctx->ek_slots = sl;
+		ctx->ek_disp = 0;
+		for (int64_t s = xfg_table_next_slot(t, -1); s >= 0; s = xfg_table_next_slot(t, s)) {
+			uint8_t k[8] = { 0 };
+			if (xfg_table_slot_key(t, (uint64_t)s, k))
+				continue;
+			uint32_t lo, hi = k[4] | (uint32_t)k[5] << 8;
+			memcpy(&lo, k, 4);
+			uint32_t e = xfg_hash_eth(lo | ((uint64_t)hi << 32), t->seed) & (sl - 1), dsp = 0;
+			while (ctx->ek_host[4 * e + 3] & XFG_EK_VALID) {
+				e = (e + 1) & (sl - 1);
+				dsp++;
+			}
+			ctx->ek_host[4 * e] = lo;
+			ctx->ek_host[4 * e + 1] = hi;
+			ctx->ek_host[4 * e + 2] = (uint32_t)s;
+			ctx->ek_host[4 * e + 3] = XFG_EK_VALID | (ctx->flag_or[2][s] & 63);
+			if (dsp > ctx->ek_disp)
+				ctx->ek_disp = dsp;
+		}
+	}
+	if (!ctx->ek_ok || d->ek_gen == ctx->ek_gen)
+		return 0;
+	pthread_mutex_lock(&d->lock);
+	if (!(err = scratch(d, (void **)&d->ek_img, &d->ek_img_bytes, (uint64_t)XFG_EK_SLOTS_MAX * 16)) &&
+	    !(err = dev_write(d, d->ek_img, ctx->ek_host, (size_t)ctx->ek_slots * 16))) {
+		d->ek_gen = ctx->ek_gen;
+		d->ek_slots = ctx->ek_slots;
+		d->ek_disp = ctx->ek_disp;
+	}
+	pthread_mutex_unlock(&d->lock);
+	return err;
+}
+
 static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b,
 		      uint8_t *verdicts, struct xfg_kargs *a)
 {
@@ -1501,6 +1574,22 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 			}
 		}
 	}
+	/* the Ethernet-key kernel (kind 6): the Ethernet-only programs, their
+	 * map as an LDS key table -- every lookup answered in LDS, no frame
+	 * byte past the two addresses read */
+	int ek = a->pipe && (ctx->prog_features & XFG_FEAT_ETHERNET) &&
+		 !(ctx->prog_features & (XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_TCP | XFG_FEAT_UDP));
+#ifdef XFG_DIAG
+	const char *eo = getenv("XFG_EK");   /* "off": the generic pipelined kernel */
+	if (eo && !strcmp(eo, "off"))
+		ek = 0;
+#endif
+	if (ek) {
+		if ((err = ek_refresh(ctx, d)))
+			return err;
+		if (ctx->ek_ok)
+			a->ek = d->ek_img;   /* (parameters: launch_batch, under d->lock) */
+	}
 	return 0;
 }
 
@@ -1562,7 +1651,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * through a handful of overfull partitions to contended atomics) */
 	const uint64_t nkeys = (uint64_t)a.t4.count + a.t6.count + a.te.count;
 	const int logged = nkeys > XFG_LOG_MIN_KEYS;
-	const int log_no = !a.pipe || !logged || a.dcnt >= a.gbase[3] || (cm && !strcmp(cm, "atomic"));
+	const int log_no = !a.pipe || !logged || a.dcnt >= a.gbase[3] || a.ek || (cm && !strcmp(cm, "atomic"));
 	/* (a batch of fewer packets than counters: the count kernel's pass over
 	 * every counter costs more than the atomics it saves -- C5's 15M + 1M
 	 * rules at 2^23 packets: 0.45 ms with atomics, 0.65-0.71 with the log;
@@ -1592,7 +1681,14 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	}
 	/* the generic pipelined kernel: small maps' Bloom filters staged in LDS */
 	a.bl_lds = 0;
-	if (a.pipe && !a.km) {
+	if (!a.pipe)   /* (header windows of the host path: the general kernel) */
+		a.ek = NULL;
+	if (a.ek) {   /* the key table in stream order at this launch */
+		a.ek = d->ek_img;
+		a.ek_slots = d->ek_slots;
+		a.ek_disp = d->ek_disp;
+	}
+	if (a.pipe && !a.km && !a.ek) {
 		const struct xfg_tdesc *tt[3] = { &a.t4, &a.te, &a.t6 };
 		uint32_t tot = 0;
 		for (int i = 0; i < 3; i++) {
@@ -1610,7 +1706,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			a.bl_lds = 0;
 #endif
 	}
-	const int kind = a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
+	const int kind = a.ek ? 6 : a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
 	if (a.qt) {   /* the index in stream order at this launch */
 		a.qt = d->qt_img;
 		a.qt_trans = d->qt_trans;
@@ -1632,7 +1728,8 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			goto out;
 		a.qt_hits = d->qt_hits;
 	}
-	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) | (a.bl_lds ? 4 : 0)];
+	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) |
+				     (a.bl_lds || a.ek ? 4 : 0)];
 #ifdef XFG_DIAG
 	const char *g = getenv("XFG_GRID_PER_CU");
 	if (g && *g)
@@ -1662,7 +1759,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.rec_port = d->rec + a.n;
 		a.rec_kb = both ? d->rec + 2 * a.n : NULL;
 	}
-	if (a.pipe) {
+	if (a.pipe && !a.ek) {   /* (the Ethernet-key kernel defers nothing) */
 		/* one deferred list per wave, room for every packet of its tiles */
 		uint64_t nw = grid * (per_wg / 64), nt = (a.n + 63) / 64;
 		uint64_t cap = (nt + nw - 1) / nw * 64;

@@ -1257,6 +1257,7 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 }
 
 #include "xfg_pipeline.hip"
+#include "xfg_pipee.hip"
 #include "xfg_pipeq.hip"
 #ifdef XFG_DIAG   // measured slower than xfg_pipe4_kernel: diagnostics only
 #include "xfg_split.hip"
@@ -1536,9 +1537,20 @@ template <uint32_t FEAT>
 hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 {
 	const size_t dl = (size_t)a.dcnt * 4 + (size_t)a.bl_lds * 4 +
-			  (a.port_nib && !a.port_tab && a.port_count ? XFG_PORT_NIB_WORDS * 4 : 0);
+			  (a.port_nib && !a.port_tab && a.port_count ? XFG_PORT_NIB_WORDS * 4 : 0) +
+			  (a.ek ? 12 + (size_t)a.ek_slots * 16 : 0);   // (+ the table's alignment)
 	if (a.pipe) {
 		bool done = false;
+		if constexpr ((FEAT & F_ETH) != 0 && (FEAT & (F_IPV4 | F_IPV6 | F_TCP | F_UDP)) == 0) {
+			// the Ethernet-only programs with their map as an LDS key table
+			if (a.ek) {
+				done = true;
+				if (a.lens_u16)
+					hipLaunchKernelGGL((xfg_pipee_kernel<FEAT, true>), dim3(grid), dim3(EK_THREADS), dl, s, a);
+				else
+					hipLaunchKernelGGL((xfg_pipee_kernel<FEAT, false>), dim3(grid), dim3(EK_THREADS), dl, s, a);
+			}
+		}
 		if constexpr ((FEAT & F_IPV4) != 0) {
 			// key mode 1 (only IPv4 keys live): the branch-free kernel
 			// (diagnostics build: or the split parse + lookup passes)
@@ -1623,19 +1635,23 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	hipError_t e;
 	switch (prog_features) {
-#ifndef XFG_AB_C3   /* (A/B variant libraries: only xdpfilt_dny_all) */
-	case F_UDP | F_DENY:              e = launch_feat<F_UDP | F_DENY>(*a, grid, s); break;
-	case F_TCP | F_DENY:              e = launch_feat<F_TCP | F_DENY>(*a, grid, s); break;
-	case F_IPV4 | F_IPV6 | F_DENY:    e = launch_feat<F_IPV4 | F_IPV6 | F_DENY>(*a, grid, s); break;
-	case F_ETH | F_DENY:              e = launch_feat<F_ETH | F_DENY>(*a, grid, s); break;
+#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)   /* (A/B variant libraries: C3's or the Ethernet programs only) */
+	case F_UDP | F_DENY:               e = launch_feat<F_UDP | F_DENY>(*a, grid, s); break;
+	case F_TCP | F_DENY:               e = launch_feat<F_TCP | F_DENY>(*a, grid, s); break;
+	case F_IPV4 | F_IPV6 | F_DENY:     e = launch_feat<F_IPV4 | F_IPV6 | F_DENY>(*a, grid, s); break;
+	case F_UDP | XFG_ALLOW:            e = launch_feat<F_UDP | XFG_ALLOW>(*a, grid, s); break;
+	case F_TCP | XFG_ALLOW:            e = launch_feat<F_TCP | XFG_ALLOW>(*a, grid, s); break;
+	case F_IPV4 | F_IPV6 | XFG_ALLOW:  e = launch_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(*a, grid, s); break;
 #endif
-	case XFG_ALL | F_DENY:            e = launch_feat<XFG_ALL | F_DENY>(*a, grid, s); break;
 #ifndef XFG_AB_C3
-	case F_UDP | XFG_ALLOW:           e = launch_feat<F_UDP | XFG_ALLOW>(*a, grid, s); break;
-	case F_TCP | XFG_ALLOW:           e = launch_feat<F_TCP | XFG_ALLOW>(*a, grid, s); break;
-	case F_IPV4 | F_IPV6 | XFG_ALLOW: e = launch_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(*a, grid, s); break;
-	case F_ETH | XFG_ALLOW:           e = launch_feat<F_ETH | XFG_ALLOW>(*a, grid, s); break;
-	case XFG_ALL | XFG_ALLOW:         e = launch_feat<XFG_ALL | XFG_ALLOW>(*a, grid, s); break;
+	case F_ETH | F_DENY:               e = launch_feat<F_ETH | F_DENY>(*a, grid, s); break;
+	case F_ETH | XFG_ALLOW:            e = launch_feat<F_ETH | XFG_ALLOW>(*a, grid, s); break;
+#endif
+#ifndef XFG_AB_ETH
+	case XFG_ALL | F_DENY:             e = launch_feat<XFG_ALL | F_DENY>(*a, grid, s); break;
+#endif
+#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)
+	case XFG_ALL | XFG_ALLOW:          e = launch_feat<XFG_ALL | XFG_ALLOW>(*a, grid, s); break;
 #endif
 	default:
 		return -22; /* -EINVAL */
@@ -1646,7 +1662,7 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 // Resident workgroups per CU of a classify kernel (persistent grid sizing)
 // with `dyn` bytes of dynamic LDS: kind 0 = general, 1 = pipelined (key
 // mode 0), 2 = pipelined (key mode 1), 5 = pipelined over the quotient
-// index; window 64 or 128.
+// index, 6 = the Ethernet-key kernel; window 64 or 128.
 template <uint32_t FEAT>
 static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 {
@@ -1707,8 +1723,20 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 			n = m;
 		}
 	}
+	if constexpr ((FEAT & F_ETH) != 0 && (FEAT & (F_IPV4 | F_IPV6 | F_TCP | F_UDP)) == 0) {
+		if (kind == 6) {   // the Ethernet-key kernel (fewest of its two length widths)
+			done = true;
+			int x = 0, y = 0;
+			e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, xfg_pipee_kernel<FEAT, true>, EK_THREADS, dyn + 12);
+			if (e == hipSuccess)
+				e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&y, xfg_pipee_kernel<FEAT, false>, EK_THREADS, dyn + 12);
+			n = x < y ? x : y;
+		}
+	}
 	if (done)
 		;
+	else if (kind == 6)
+		n = 1;   // (no such kernel for this program: never launched)
 	else if (kind >= 1)
 		e = window <= 64
 			? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipeline_kernel<FEAT, 64, true, 0>, PIPE_THREADS(64), dyn)
@@ -1723,19 +1751,23 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 extern "C" int xfg_classify_occupancy(uint32_t prog_features, int kind, uint32_t window, size_t dyn)
 {
 	switch (prog_features) {
-#ifndef XFG_AB_C3   /* (A/B variant libraries: only xdpfilt_dny_all) */
-	case F_UDP | F_DENY:              return occupancy_feat<F_UDP | F_DENY>(kind, window, dyn);
-	case F_TCP | F_DENY:              return occupancy_feat<F_TCP | F_DENY>(kind, window, dyn);
-	case F_IPV4 | F_IPV6 | F_DENY:    return occupancy_feat<F_IPV4 | F_IPV6 | F_DENY>(kind, window, dyn);
-	case F_ETH | F_DENY:              return occupancy_feat<F_ETH | F_DENY>(kind, window, dyn);
+#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)   /* (A/B variant libraries: C3's or the Ethernet programs only) */
+	case F_UDP | F_DENY:               return occupancy_feat<F_UDP | F_DENY>(kind, window, dyn);
+	case F_TCP | F_DENY:               return occupancy_feat<F_TCP | F_DENY>(kind, window, dyn);
+	case F_IPV4 | F_IPV6 | F_DENY:     return occupancy_feat<F_IPV4 | F_IPV6 | F_DENY>(kind, window, dyn);
+	case F_UDP | XFG_ALLOW:            return occupancy_feat<F_UDP | XFG_ALLOW>(kind, window, dyn);
+	case F_TCP | XFG_ALLOW:            return occupancy_feat<F_TCP | XFG_ALLOW>(kind, window, dyn);
+	case F_IPV4 | F_IPV6 | XFG_ALLOW:  return occupancy_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(kind, window, dyn);
 #endif
-	case XFG_ALL | F_DENY:            return occupancy_feat<XFG_ALL | F_DENY>(kind, window, dyn);
 #ifndef XFG_AB_C3
-	case F_UDP | XFG_ALLOW:           return occupancy_feat<F_UDP | XFG_ALLOW>(kind, window, dyn);
-	case F_TCP | XFG_ALLOW:           return occupancy_feat<F_TCP | XFG_ALLOW>(kind, window, dyn);
-	case F_IPV4 | F_IPV6 | XFG_ALLOW: return occupancy_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(kind, window, dyn);
-	case F_ETH | XFG_ALLOW:           return occupancy_feat<F_ETH | XFG_ALLOW>(kind, window, dyn);
-	case XFG_ALL | XFG_ALLOW:         return occupancy_feat<XFG_ALL | XFG_ALLOW>(kind, window, dyn);
+	case F_ETH | F_DENY:               return occupancy_feat<F_ETH | F_DENY>(kind, window, dyn);
+	case F_ETH | XFG_ALLOW:            return occupancy_feat<F_ETH | XFG_ALLOW>(kind, window, dyn);
+#endif
+#ifndef XFG_AB_ETH
+	case XFG_ALL | F_DENY:             return occupancy_feat<XFG_ALL | F_DENY>(kind, window, dyn);
+#endif
+#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)
+	case XFG_ALL | XFG_ALLOW:          return occupancy_feat<XFG_ALL | XFG_ALLOW>(kind, window, dyn);
 #endif
 	default:                          return 1;
 	}
@@ -1748,6 +1780,8 @@ extern "C" int xfg_classify_threads(int kind, uint32_t window)
 		return 256;   // the split parse pass (diagnostics build)
 	if (kind == 5)
 		return window <= 64 ? QT_THREADS(64) : QT_THREADS(128);
+	if (kind == 6)
+		return EK_THREADS;
 	return kind >= 1 ? (window <= 64 ? PIPE_THREADS(64) : PIPE_THREADS(128)) : TILE;
 }
 

@@ -96,6 +96,9 @@
 #define XFG_QT_OVF_MARK   0x0001u /* entry 15: the bucket overflowed */
 
 #define XFG_DCNT_MAX      4096u   /* direct LDS counters (16 KiB) */
+#define XFG_EK_SLOTS_MAX  1024u   /* Ethernet-key kernel: LDS key table entries (16 KiB) */
+#define XFG_EK_MAX_KEYS   512u    /* ... at most this many keys (half the entries) */
+#define XFG_EK_VALID      0x100u  /* an occupied entry (beside the flag byte) */
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
 #define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
 #define XFG_LOG_PASSES_MAX 32u    /* histogram passes per partition (span 512K) */
@@ -171,6 +174,15 @@ struct xfg_kargs {
 	 * the words read from memory */
 	uint32_t bl_lds;
 	uint32_t bl_off[3];
+	/* The Ethernet-key kernel (xdpfilt_{alw,dny}_eth; a map of at most
+	 * XFG_EK_MAX_KEYS keys whose flags agree on every device): the map as an
+	 * open-addressed table of ek_slots (a power of two) 16-byte entries
+	 * {MAC bytes 0-3, bytes 4-5, slot, flags | XFG_EK_VALID}, copied to LDS
+	 * by every workgroup; a key sits at most ek_disp entries past its home
+	 * (xfg_hash_eth & (ek_slots - 1)).  NULL: not this kernel. */
+	const uint32_t *ek;
+	uint32_t ek_slots;
+	uint32_t ek_disp;
 	/* Hit log of the pipelined kernels (tlog NULL = no log): per-wave
 	 * regions of defer_cap counter identities; partition-major buffer of
 	 * XFG_LOG_PARTS x pslices slices of pcap entries, slice (p, b) owned by
