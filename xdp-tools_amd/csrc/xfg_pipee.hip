@@ -22,11 +22,17 @@
 // A wave takes G tiles of 64 packets per iteration (one packet per lane per
 // tile; tiles dealt over the grid's waves as in the other pipelined kernels,
 // so a wave's share is the same), their first 16 bytes and lengths loaded
-// one iteration ahead into the other of two register buffers.
+// D - 1 iterations ahead into a ring of D register buffers.
 namespace {
 
+// (C1, one box, profiles/r05_s22_session.log and r05_s23_session.log: G 1
+// and D 2 0.185 ms at 2^24; G 2 0.190-0.201, G 4 0.209, G 8 0.258; D 3 and
+// 4 and 8 waves a SIMD slower -- the smaller loop body wins)
 #ifndef XFG_EK_G   /* tiles per wave iteration */
-#define XFG_EK_G 4
+#define XFG_EK_G 1
+#endif
+#ifndef XFG_EK_D   /* register buffers of G tiles each */
+#define XFG_EK_D 2
 #endif
 #define EK_WAVES 8
 #define EK_THREADS (64 * EK_WAVES)
@@ -45,7 +51,7 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 {
 	static_assert((FEAT & F_ETH) != 0 && (FEAT & (F_IPV4 | F_IPV6 | F_TCP | F_UDP)) == 0,
 		      "the Ethernet-key kernel runs the Ethernet-only programs");
-	constexpr int NW = EK_WAVES, NT = EK_THREADS, G = XFG_EK_G;
+	constexpr int NW = EK_WAVES, NT = EK_THREADS, G = XFG_EK_G, D = XFG_EK_D;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
@@ -151,21 +157,27 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 		}
 	};
 
-	u32x4 fA[G], fB[G];
-	uint32_t lA[G], lB[G];
+	// D register buffers: group g in buffer g % D, D - 1 groups in flight
+	// while one is processed
+	u32x4 fb[D][G];
+	uint32_t lb[D][G];
 	if (ng) {
-		issue(0, fA, lA);
-		issue(1, fB, lB);
+#pragma unroll
+		for (int d = 0; d < D; d++)
+			issue(d, fb[d], lb[d]);
 	}
 	uint32_t g = 0;
-	for (; g + 1 < ng; g += 2) {
-		process(g, fA, lA);
-		issue(g + 2, fA, lA);
-		process(g + 1, fB, lB);
-		issue(g + 3, fB, lB);
+	for (; g + D <= ng; g += D) {
+#pragma unroll
+		for (int d = 0; d < D; d++) {
+			process(g + d, fb[d], lb[d]);
+			issue(g + d + D, fb[d], lb[d]);
+		}
 	}
-	if (g < ng)
-		process(g, fA, lA);
+#pragma unroll
+	for (int d = 0; d < D - 1; d++)
+		if (g + d < ng)
+			process(g + d, fb[d], lb[d]);
 
 	const uint32_t vb[3] = { st_b0, st_b1, st_b2 }, vc[3] = { st_c0, st_c1, st_c2 };
 #pragma unroll

@@ -52,6 +52,9 @@
 #ifndef XFG_QT_OWNC      /* a wave owns PPW consecutive log partitions (0: every NW-th) */
 #define XFG_QT_OWNC 1
 #endif
+#ifndef XFG_QT_LANEW     /* (A/B) each lane loads its own frame's window: no LDS rows */
+#define XFG_QT_LANEW 0
+#endif
 #ifndef XFG_QT_ROWQ      /* rows of 16-byte-aligned stride: b128 LDS writes and reads (0: b32) */
 #define XFG_QT_ROWQ 1
 #endif
@@ -126,6 +129,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr bool ROWQ = XFG_QT_ROWQ != 0;
 	constexpr int ROWDW = ROWQ ? W / 4 + 4 : W / 4 + 1;
 	constexpr int NQ = W >= 68 ? 5 : 4;   // (ROWQ) the row's first 16-byte pieces the parse reads
+	// (LANEW, 64-byte windows: lane L's four loads are its own frame's
+	// window, parsed from registers -- no row staging, strided loads)
+	constexpr bool LANEW = XFG_QT_LANEW != 0 && W == 64;
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t LAG = XFG_QT_LAG;
@@ -271,15 +277,16 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
 				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
-				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
-							 : reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
+				const u32x4 *src = LANEW ? reinterpret_cast<const u32x4 *>(tb + (uint32_t)lane * (DENSE ? W : a.stride) + it * 16)
+					: DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
+						: reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
 				pre[it] = __builtin_nontemporal_load(src);
 			}
 			plen = ld_len(lb + ((uint64_t)base << lsh) + ((uint32_t)lane << lsh));
 		} else {
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
-				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
+				const uint32_t c = it * 64 + lane, pk = LANEW ? (uint32_t)lane : c / CPP, sub = LANEW ? (uint32_t)it : c % CPP;
 				const uint32_t q = pk < rem ? pk : 0u;
 				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + (q * CPP + sub)
 							 : reinterpret_cast<const u32x4 *>(a.data + (uint64_t)(base + q) * a.stride + sub * 16);
@@ -748,7 +755,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		if (vP) {
 			const uint32_t rem = n - tP * 64 >= 64 ? 64u : n - tP * 64;
 			__builtin_amdgcn_wave_barrier();
-			if (!(dg & 32)) {
+			if (LANEW) {
+				;   // (the window stays in registers)
+			} else if (!(dg & 32)) {
 #pragma unroll
 				for (int it = 0; it < CPP; it++) {
 					const int c = it * 64 + lane;
@@ -783,7 +792,15 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		// (a shared line).
 		uint32_t hk = 0, lbk = 0, hk2 = 0, lbk2 = 0;
 		uint32_t dw[17] = {};   // (ROWQ) the row's dwords, read four at a time
-		if constexpr (ROWQ) {
+		if constexpr (LANEW) {
+#pragma unroll
+			for (int q = 0; q < CPP; q++) {
+				dw[4 * q] = cur[q].x;
+				dw[4 * q + 1] = cur[q].y;
+				dw[4 * q + 2] = cur[q].z;
+				dw[4 * q + 3] = cur[q].w;
+			}
+		} else if constexpr (ROWQ) {
 			if (vP) {
 #pragma unroll
 				for (int q = 0; q < NQ; q++) {
@@ -798,7 +815,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				}
 			}
 		}
-		auto rowd = [&](int j) { return ROWQ ? dw[j] : myrow[j]; };
+		auto rowd = [&](int j) { return (ROWQ || LANEW) ? dw[j] : myrow[j]; };
 		if (vP) {
 			const uint32_t e3 = rowd(3), e6 = rowd(6), e7 = rowd(7), e8 = rowd(8);
 			const uint32_t key = dlive ? __builtin_amdgcn_alignbyte(e8, e7, 2) : __builtin_amdgcn_alignbyte(e7, e6, 2);
@@ -841,7 +858,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		} else if (vP) {
 			const uint32_t gi = tP * 64 + lane;
 			Parse4 r;
-			if constexpr (ROWQ)
+			if constexpr (ROWQ || LANEW)
 				r = parse_bf_dw<FEAT, W>(dw, len);
 			else
 				r = parse_bf<FEAT, W>(myrow, len);
