@@ -137,7 +137,7 @@ def run(name, args):
                          "achieved_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "setup_s": round(setup_s, 1)}
-    if kind == 5:
+    if kind == 5 and not args.no_host:
         # end to end from host memory: whole frames and lengths H2D, verdicts D2H
         f.classify_host(data, lens, stride=stride)
         t1 = time.perf_counter()
@@ -179,6 +179,8 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c2", "c4", "c5", "c3sd"])
     ap.add_argument("--log2-packets", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true", help="c1: the GPU leg only")
+    ap.add_argument("--no-host", action="store_true",
+                    help="c5: the device-resident leg only (PMC passes of its kernel)")
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     for c in a.configs:
