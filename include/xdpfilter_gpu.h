@@ -119,12 +119,14 @@ const char *xfg_strerror(int err);
 /* The classify kernel the last launch on device @dev ran (introspection for
  * tests and tools): XFG_PATH_GENERAL (offsets, descriptors, header
  * windows), _PIPELINE (fixed stride, any live key), _IPV4 (IPv4 keys only:
- * prefilter + bucket line), _QT (IPv4 keys only: the quotient index); or
+ * prefilter + bucket line), _QT (IPv4 keys only: the quotient index),
+ * _ETH (the Ethernet-only programs, their map as an LDS key table); or
  * -EINVAL / -ENOENT (no launch yet). */
 #define XFG_PATH_GENERAL  0
 #define XFG_PATH_PIPELINE 1
 #define XFG_PATH_IPV4     2
 #define XFG_PATH_QT       5
+#define XFG_PATH_ETH      6
 int xfg_last_path(const xfg_ctx *ctx, int dev);
 
 /*

@@ -543,3 +543,32 @@ def test_classify_host_registered_slices(G, stride, first):
     np.testing.assert_array_equal(v, ov)
     np.testing.assert_array_equal(f.stats(), ost)
     f.close()
+
+
+def test_classify_host_registered_large_slots_many_frames(G):
+    """Registered 1536-byte slots, 798k frames read in place (zero copy)
+    with the 15-bit-remainder index off (500 rules) and IPv6 frames whose
+    program walks past the 64-byte window (the kernels' deferred walk reads
+    the mapped frame) -- every frame's verdict, every counter and the
+    stats equal the restatement's."""
+    stride = 1536
+    n = (1 << 19) + (1 << 18) + 12345
+    rules, pool = X.random_rules(404, n4=500, n6=200, ne=30, nports=40)
+    data, lens = X.gen_fuzz(405, n, stride, rules, pool)
+    feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    ov, orules, ost = X.run_oracle(feats, data, lens, rules, stride=stride, nthreads=8)
+    f = G.Filter(feats, ndev=1)
+    f.load_rules(rules)
+    f.host_register(data)
+    try:
+        v = f.classify_host(data, lens, stride=stride)
+    finally:
+        f.host_unregister(data)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(f.stats(), ost)
+    r = rules.prepared()
+    np.testing.assert_array_equal(f.values_of(G.MAP_IPV4, r.v4_keys), orules.v4_vals)
+    np.testing.assert_array_equal(f.values_of(G.MAP_IPV6, r.v6_keys), orules.v6_vals)
+    np.testing.assert_array_equal(f.values_of(G.MAP_PORTS, np.arange(65536, dtype=np.uint32)),
+                                  orules.ports)
+    f.close()

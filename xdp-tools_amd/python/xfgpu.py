@@ -499,7 +499,7 @@ class Filter:
     def stats_reset(self):
         _check(lib.xfg_stats_reset(self.ctx), "stats_reset")
 
-    PATH_GENERAL, PATH_PIPELINE, PATH_IPV4, PATH_QT = 0, 1, 2, 5
+    PATH_GENERAL, PATH_PIPELINE, PATH_IPV4, PATH_QT, PATH_ETH = 0, 1, 2, 5, 6
 
     def last_path(self, dev=0) -> int:
         """The classify kernel of the last launch on @dev (xfg_last_path)."""
