@@ -547,7 +547,7 @@ def test_classify_host_registered_slices(G, stride, first):
 
 def test_classify_host_registered_large_slots_many_frames(G):
     """Registered 1536-byte slots, 798k frames read in place (zero copy)
-    with the 15-bit-remainder index off (500 rules) and IPv6 frames whose
+    (500 rules: the generic pipelined kernel) and IPv6 frames whose
     program walks past the 64-byte window (the kernels' deferred walk reads
     the mapped frame) -- every frame's verdict, every counter and the
     stats equal the restatement's."""

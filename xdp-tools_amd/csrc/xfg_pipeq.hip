@@ -52,6 +52,9 @@
 #ifndef XFG_QT_OWNC      /* a wave owns PPW consecutive log partitions (0: every NW-th) */
 #define XFG_QT_OWNC 1
 #endif
+#ifndef XFG_QT_SWZ       /* (A/B) lanes 8g..8g+7 carry one 16-byte piece of 8 packets */
+#define XFG_QT_SWZ 0
+#endif
 #ifndef XFG_QT_LANEW     /* (A/B) each lane loads its own frame's window: no LDS rows */
 #define XFG_QT_LANEW 0
 #endif
@@ -132,6 +135,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// (LANEW, 64-byte windows: lane L's four loads are its own frame's
 	// window, parsed from registers -- no row staging, strided loads)
 	constexpr bool LANEW = XFG_QT_LANEW != 0 && W == 64;
+	// (SWZ, 64-byte windows: lane L of load it carries piece (L >> 3) & 3 of
+	// packet 16 it + 8 (L >> 5) + (L & 7) -- the same kilobyte, so that each
+	// group of 8 lanes of the row store writes one piece of 8 consecutive
+	// rows, whose banks are disjoint at the 20-dword row stride)
+	constexpr bool SWZ = XFG_QT_SWZ != 0 && W == 64 && !LANEW;
 	constexpr bool PORTS = (FEAT & (F_UDP | F_TCP)) != 0;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t LAG = XFG_QT_LAG;
@@ -219,6 +227,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	constexpr uint32_t dg = 0;
 #endif
 	const int tid = threadIdx.x, lane = tid & 63;
+	auto piece = [&](int it, uint32_t &pk, uint32_t &sub) {
+		const uint32_t c = it * 64 + (uint32_t)lane;
+		pk = SWZ ? it * 16 + ((uint32_t)lane >> 5) * 8 + ((uint32_t)lane & 7) : c / CPP;
+		sub = SWZ ? ((uint32_t)lane >> 3) & 3 : c % CPP;
+	};
 	const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 	// the index, in scalar registers
 	const uint64_t qb = rfl64((uint64_t)(uintptr_t)a.qt);
@@ -276,9 +289,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			const uint8_t *tb = a.data + (uint64_t)base * (DENSE ? W : a.stride);
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
-				const uint32_t c = it * 64 + lane, pk = c / CPP, sub = c % CPP;
+				uint32_t pk, sub;
+				piece(it, pk, sub);
 				const u32x4 *src = LANEW ? reinterpret_cast<const u32x4 *>(tb + (uint32_t)lane * (DENSE ? W : a.stride) + it * 16)
-					: DENSE ? reinterpret_cast<const u32x4 *>(tb) + c
+					: DENSE ? reinterpret_cast<const u32x4 *>(tb) + (pk * CPP + sub)
 						: reinterpret_cast<const u32x4 *>(tb + pk * a.stride + sub * 16);
 				pre[it] = __builtin_nontemporal_load(src);
 			}
@@ -286,7 +300,12 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		} else {
 #pragma unroll
 			for (int it = 0; it < CPP; it++) {
-				const uint32_t c = it * 64 + lane, pk = LANEW ? (uint32_t)lane : c / CPP, sub = LANEW ? (uint32_t)it : c % CPP;
+				uint32_t pk, sub;
+				piece(it, pk, sub);
+				if (LANEW) {
+					pk = (uint32_t)lane;
+					sub = (uint32_t)it;
+				}
 				const uint32_t q = pk < rem ? pk : 0u;
 				const u32x4 *src = DENSE ? reinterpret_cast<const u32x4 *>(a.data + (uint64_t)base * W) + (q * CPP + sub)
 							 : reinterpret_cast<const u32x4 *>(a.data + (uint64_t)(base + q) * a.stride + sub * 16);
@@ -761,7 +780,9 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 #pragma unroll
 				for (int it = 0; it < CPP; it++) {
 					const int c = it * 64 + lane;
-					const int pk = c / CPP, sub = c % CPP;
+					uint32_t pk, sub;
+					piece(it, pk, sub);
+					(void)c;
 					uint32_t *dst = &rows[pk * ROWDW + sub * 4];
 					if constexpr (ROWQ) {
 						*reinterpret_cast<u32x4 *>(dst) = cur[it];
