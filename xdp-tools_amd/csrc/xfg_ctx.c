@@ -17,6 +17,7 @@
 #include <errno.h>
 #include <stddef.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -262,8 +263,29 @@ static int keylen_of(int map)
 
 /* ------------------------------------------------------------------ gather pool */
 /* Persistent worker threads of one device's host path: hpool_run(fn, arg)
- * runs fn(arg, slice, nslices) for every slice, slice 0 on the caller. */
-#define HOST_THREADS 8
+ * runs fn(arg, slice, nslices) for every slice, slice 0 on the caller.  As
+ * many as the process's CPU set allows, capped by OMP_NUM_THREADS when set
+ * (a shared box's CPU share: its CPU set shows the whole machine) and by
+ * HOST_THREADS (performance only: the slices' results do not depend on
+ * their count). */
+#define HOST_THREADS 16
+
+static int hpool_size(void)
+{
+	int n = HOST_THREADS;
+	cpu_set_t cs;
+	if (!sched_getaffinity(0, sizeof(cs), &cs) && CPU_COUNT(&cs) > 0 && CPU_COUNT(&cs) < n)
+		n = CPU_COUNT(&cs);
+	const char *omp = getenv("OMP_NUM_THREADS");
+	if (omp && atoi(omp) > 0 && atoi(omp) < n)
+		n = atoi(omp);
+#ifdef XFG_DIAG
+	const char *ht = getenv("XFG_HOST_THREADS");   /* gather threads (round 4: 8) */
+	if (ht && atoi(ht) > 0 && atoi(ht) <= HOST_THREADS)
+		n = atoi(ht);
+#endif
+	return n;
+}
 
 struct hpool {
 	pthread_t th[HOST_THREADS];
@@ -314,8 +336,9 @@ static struct hpool *hpool_start(void)
 	pthread_cond_init(&p->go, NULL);
 	pthread_cond_init(&p->done, NULL);
 	/* (workers are told their count under the lock, before any run) */
+	const int nt = hpool_size();
 	pthread_mutex_lock(&p->mu);
-	for (int t = 1; t < HOST_THREADS; t++) {
+	for (int t = 1; t < nt; t++) {
 		p->args[t] = (struct hpool_arg){ p, t };
 		if (pthread_create(&p->th[t], NULL, hpool_main, &p->args[t]))
 			break;
