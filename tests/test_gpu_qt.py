@@ -19,6 +19,8 @@ in two count passes.  The kernel logs its hits only for batches of at least
 as many packets as the index has slots (xfg_ctx.c launch_batch); the
 smaller batches here count through its LDS counter cache and atomics.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -593,3 +595,20 @@ def test_qt_window_128_option(G, stride):
     data = np.concatenate([d1, d2])
     lens = np.concatenate([l1, l2])
     run_both(G, "xdpfilt_dny_all", rules, data, lens, stride, ipv6_capacity=1 << 13, window=128)
+
+
+@pytest.mark.timeout(300)
+def test_qt_counts_folded_before_32_bits():
+    """The QT-order hit counts are 32-bit (xfg_kargs.qt_hits): the runtime
+    folds them into the canonical 64-bit counters before the packets
+    classified since the last fold could overflow one. Run in a fresh
+    process on the diagnostics library with the fold threshold lowered to
+    100,000 packets, so that folds are queued between the launches of one
+    timed classify, with and without the hit log: every rule's value and the
+    stats equal the oracle's figures for the same number of passes."""
+    import subprocess
+    import sys
+    env = dict(os.environ, XFG_LIB="diag", XFG_QT_FOLD_AT="100000")
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gpu_fold_worker.py"), "5"],
+                       capture_output=True, text=True, timeout=280, env=env)
+    assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]

@@ -40,7 +40,7 @@ int xfg_launch_compact(const uint8_t *verdicts, uint64_t n, uint32_t action, uin
 		       unsigned long long *count, unsigned long long *status, uint32_t *ticket,
 		       unsigned grid, void *stream);
 uint64_t xfg_compact_tiles(uint64_t n);
-int xfg_launch_qt_fold(unsigned long long *qt_hits, const uint32_t *trans,
+int xfg_launch_qt_fold(uint32_t *qt_hits, const uint32_t *trans,
 		       unsigned long long *hits, uint32_t n, void *stream);
 
 #define NMAPS_HASH 3 /* ipv4, ipv6, ethernet */
@@ -99,8 +99,9 @@ struct xfg_dev {
 	uint32_t qt_gen, qt_bits, qt_seed, qt_live, qt_n, qt_nimg;
 	/* the count kernel's QT-order hit counts (xfg_kargs.qt_hits) and
 	 * whether a launch may have added to them since the last fold */
-	unsigned long long *qt_hits;
+	uint32_t *qt_hits;
 	uint64_t qt_hits_bytes;
+	uint64_t qt_pk;                /* packets classified through the index since the last fold */
 	int qt_pending;
 	int last_kind;                 /* kernel kind of the last launch (-1: none) */
 	/* host-resident classify (xfg_classify_host / xfg_classify_xsk_host),
@@ -692,8 +693,23 @@ static int qt_fold_locked(struct xfg_dev *d)
 		err = xfg_launch_qt_fold(d->qt_hits, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
 	if (!err)
 		err = hip_err(hipStreamSynchronize(d->stream));
-	if (!err)
+	if (!err) {
 		d->qt_pending = 0;
+		d->qt_pk = 0;
+	}
+	return err;
+}
+
+/* The same fold queued on the device stream with no wait (d->lock held):
+ * before a launch whose packets could take a 32-bit QT-order count past
+ * 2^32 - 1 (xfg_kargs.qt_hits). */
+static int qt_fold_queued(struct xfg_dev *d)
+{
+	int err = log_flush_locked(d);
+	if (!err)
+		err = xfg_launch_qt_fold(d->qt_hits, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
+	if (!err)
+		d->qt_pk = 0;
 	return err;
 }
 
@@ -1743,7 +1759,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.qt2 = d->qt_img + (uint64_t)a.qt_base * 2 / 4;
 		/* its QT-order counts (zeroed when (re)allocated; a resize only
 		 * follows a fold: qt_refresh) */
-		const uint64_t qb = (uint64_t)d->qt_n * 8, had = d->qt_hits_bytes;
+		const uint64_t qb = (uint64_t)d->qt_n * 4, had = d->qt_hits_bytes;
 		if ((err = scratch(d, (void **)&d->qt_hits, &d->qt_hits_bytes, qb)))
 			goto out;
 		if (d->qt_hits_bytes != had &&
@@ -1894,7 +1910,18 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * count kernel on a second stream, overlapped with the next classify,
 	 * shares the CUs and slowed the classify more than it hid:
 	 * profiles/r04_s11_count_overlap.log) */
+	uint64_t fold_at = 0xffffffffull;   /* (a 32-bit QT-order count's room) */
+#ifdef XFG_DIAG
+	const char *fa = getenv("XFG_QT_FOLD_AT");   /* tests: fold after this many packets */
+	if (fa && strtoull(fa, NULL, 0))
+		fold_at = strtoull(fa, NULL, 0);
+#endif
 	for (int i = 0; i < iters && !err; i++) {
+		if (a.qt_hits) {
+			if (d->qt_pk + a.n > fold_at && (err = qt_fold_queued(d)))
+				break;
+			d->qt_pk += a.n;
+		}
 		if (a.pbuf && K > 1)
 			a.pslice0 = d->log_pend * (uint32_t)grid;
 		err = xfg_launch_classify(ctx->prog_features, &a, (unsigned)grid, d->stream);

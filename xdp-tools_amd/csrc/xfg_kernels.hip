@@ -748,22 +748,27 @@ __device__ __forceinline__ bool cache_hit(uint32_t *s_ctag, uint32_t *s_ccnt, ui
 // Word w of packet i's AF_XDP descriptor (ring index wraps with desc_mask).
 __device__ __forceinline__ uint64_t desc_word(const xfg_kargs &a, uint64_t i, int w)
 {
-	return a.descs[2ull * ((a.desc_first + (uint32_t)i) & a.desc_mask) + w];
+	return reinterpret_cast<const __attribute__((address_space(1))) uint64_t *>(
+		reinterpret_cast<uintptr_t>(a.descs))[2ull * ((a.desc_first + (uint32_t)i) & a.desc_mask) + w];
 }
 
 // Length of packet i in the pipelined kernels' layout (no descriptors).
+// (through the global address space: a FLAT load would also count against
+// the LDS counter, and the loops' LDS waits would wait for it)
 __device__ __forceinline__ uint32_t load_len_fixed(const xfg_kargs &a, uint32_t i)
 {
-	return a.lens_u16 ? static_cast<const uint16_t *>(a.lens)[i]
-			  : static_cast<const uint32_t *>(a.lens)[i];
+	const uintptr_t p = reinterpret_cast<uintptr_t>(a.lens);
+	return a.lens_u16 ? reinterpret_cast<const __attribute__((address_space(1))) uint16_t *>(p)[i]
+			  : reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(p)[i];
 }
 
 __device__ __forceinline__ uint32_t load_len(const xfg_kargs &a, uint64_t i)
 {
 	if (a.descs)
 		return (uint32_t)desc_word(a, i, 1);   // xdp_desc.len (low half, little-endian)
-	return a.lens_u16 ? static_cast<const uint16_t *>(a.lens)[i]
-			  : static_cast<const uint32_t *>(a.lens)[i];
+	const uintptr_t p = reinterpret_cast<uintptr_t>(a.lens);
+	return a.lens_u16 ? reinterpret_cast<const __attribute__((address_space(1))) uint16_t *>(p)[i]
+			  : reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(p)[i];
 }
 
 __device__ __forceinline__ const uint8_t *pkt_ptr(const xfg_kargs &a, uint64_t i)
@@ -775,6 +780,15 @@ __device__ __forceinline__ const uint8_t *pkt_ptr(const xfg_kargs &a, uint64_t i
 		return a.data + (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	}
 	return a.data + (a.offsets ? a.offsets[i] : i * (uint64_t)a.stride);
+}
+
+// A 32-bit atomic add through the global address space (atomicAdd on a
+// generic pointer may become a FLAT atomic, which counts against the LDS
+// counter as well: the loop's LDS waits would wait for it)
+__device__ __forceinline__ void gatomic_add32(uint32_t *p, uint32_t v)
+{
+	__hip_atomic_fetch_add(reinterpret_cast<__attribute__((address_space(1))) uint32_t *>((uintptr_t)p), v,
+			       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- counters and stats
@@ -834,9 +848,12 @@ struct Counters {
 	__device__ __forceinline__ void flush(const xfg_kargs &a, int tid, int nthr)
 	{
 		for (int i = tid; i < CC_ENTRIES; i += nthr)
-			if (ctag[i] != CT_NONE && ccnt[i])
-				atomicAdd((ctag[i] & CT_QTAG) ? a.qt_hits + (ctag[i] & ~CT_QTAG) : global_counter(a, ctag[i]),
-					  (unsigned long long)ccnt[i]);
+			if (ctag[i] != CT_NONE && ccnt[i]) {
+				if (ctag[i] & CT_QTAG)
+					gatomic_add32(a.qt_hits + (ctag[i] & ~CT_QTAG), ccnt[i]);
+				else
+					atomicAdd(global_counter(a, ctag[i]), (unsigned long long)ccnt[i]);
+			}
 		for (uint32_t i = tid; i < a.dcnt; i += nthr)
 			if (dcnt[i])
 				atomicAdd(global_counter(a, i), (unsigned long long)dcnt[i]);
@@ -1291,7 +1308,6 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	// (the quotient index: the QT-order counts, 16 slots a line)
 	uint32_t gid[J];
 	unsigned long long val[J];
-	auto ctr = [&](uint32_t g) { return a.qt_hits ? a.qt_hits + g : global_counter(a, g); };
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++) {
 		const uint32_t k = tid + j * LC_THREADS, l = j0 + k;
@@ -1309,7 +1325,8 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 #endif
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++)
-		val[j] = gid[j] != CT_NONE && !normw ? *ctr(gid[j]) : 0ull;
+		val[j] = gid[j] == CT_NONE || normw ? 0ull
+			 : a.qt_hits ? (unsigned long long)a.qt_hits[gid[j]] : *global_counter(a, gid[j]);
 	if (tid < S)
 		s_fill[tid] = min(fl, cap);
 	__syncthreads();
@@ -1377,8 +1394,12 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++) {
 		const uint32_t k = tid + j * LC_THREADS;
-		if (gid[j] != CT_NONE && hist[k] && !normw)
-			*ctr(gid[j]) = val[j] + hist[k];
+		if (gid[j] != CT_NONE && hist[k] && !normw) {
+			if (a.qt_hits)
+				a.qt_hits[gid[j]] = (uint32_t)(val[j] + hist[k]);
+			else
+				*global_counter(a, gid[j]) = val[j] + hist[k];
+		}
 	}
 }
 
@@ -1810,12 +1831,12 @@ extern "C" int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sin
 // Fold the QT-order hit counts into the canonical IPv4 counters (qt_trans
 // is injective: each canonical counter has at most one QT slot, so a plain
 // read-modify-write) and zero them.  Runs at readout, not per batch.
-__global__ __launch_bounds__(256) void xfg_qt_fold_kernel(unsigned long long *__restrict__ qh,
+__global__ __launch_bounds__(256) void xfg_qt_fold_kernel(uint32_t *__restrict__ qh,
 							  const uint32_t *__restrict__ trans,
 							  unsigned long long *__restrict__ hits, uint32_t n)
 {
 	for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < n; q += gridDim.x * 256u) {
-		const unsigned long long v = qh[q];
+		const uint32_t v = qh[q];
 		if (v) {
 			const uint32_t c = trans[q];
 			if (c != CT_NONE)
@@ -1825,7 +1846,7 @@ __global__ __launch_bounds__(256) void xfg_qt_fold_kernel(unsigned long long *__
 	}
 }
 
-extern "C" int xfg_launch_qt_fold(unsigned long long *qt_hits, const uint32_t *trans,
+extern "C" int xfg_launch_qt_fold(uint32_t *qt_hits, const uint32_t *trans,
 				  unsigned long long *hits, uint32_t n, void *stream)
 {
 	const uint32_t grid = n ? (n + 255) / 256 < 2048u ? (n + 255) / 256 : 2048u : 1u;

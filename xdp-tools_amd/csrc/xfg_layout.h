@@ -251,8 +251,12 @@ struct xfg_kargs {
 	/* hit counts of the QT slots (qt_n, QT-slot order): the count kernel
 	 * adds there, the host folds them into the canonical counters through
 	 * qt_trans before any counter read, write or re-index (the per-CPU
-	 * counters of BPF are summed at readout the same way) */
-	unsigned long long *qt_hits;
+	 * counters of BPF are summed at readout the same way); 32-bit: the
+	 * host folds them too before the packets classified since the last
+	 * fold could reach 2^32 (a packet bumps at most one), which keeps the
+	 * array half the size -- C5's 2^25 QT slots in 128 MB, inside the
+	 * Infinity Cache -- for the kernels' atomics */
+	uint32_t *qt_hits;
 	uint32_t qt_bits;
 	uint32_t qt_seed;
 	uint32_t qt_base;

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 					if (ql & !ok)
 						atomicSub(&s_res[p], 1u);
 					if ((q & !ok) && !cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
-						atomicAdd(a.qt_hits + qs, 1ull);
+						gatomic_add32(a.qt_hits + qs, 1u);
 					if (dc & !ps)
 						atomicAdd(&cn.dcnt[tag], 1u);
 					cn.bump(a, pick(q | dc | ps, CT_NONE, tag), lane);
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				}
 				// the ring full (or no log): the LDS counter cache
 				if (!ring && !cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
-					atomicAdd(a.qt_hits + qs, 1ull);
+					gatomic_add32(a.qt_hits + qs, 1u);
 			}
 		}
 		if constexpr (PORTS)
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			} else {
 				const uint32_t g = ((e >> 4) << 12) | (p << 4) | (e & 15);
 				if (!cache_hit(cn.ctag, cn.ccnt, QTAG | g, 1))
-					atomicAdd(a.qt_hits + g, 1ull);
+					gatomic_add32(a.qt_hits + g, 1u);
 			}
 		}
 	};

@@ -26,7 +26,8 @@ except Exception:  # torch absent: the library uses /opt/rocm's runtime
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# XFG_LIB=diag selects the diagnostics build (measurement knobs; tools/ only),
+# XFG_LIB=diag selects the diagnostics build (measurement knobs; tools/, and the
+# test that lowers the QT fold threshold),
 # XFG_LIB=asan the sanitizer build of the host C (the CPU suite under
 # tools/asan_suite.sh)
 # tools/ A/B runs may also name a library file outright (XFG_LIB=/path/x.so)
