@@ -31,7 +31,7 @@ def main():
     ports = np.array([53, 80], np.uint16)
     for p in ports:
         rules.ports[X.port_key(int(p))] = 2 | 4 | 8
-    for n in (1 << 16, 1 << 21):   # (below the QT slots, 2^21: no log, atomics; at them: the log)
+    for n in (1 << 16, 1 << 22):   # (2^21 QT slots: below twice them no log, atomics; at twice: the log)
         data, lens = X.gen_workload(7, 3, n, 64, v4=v4, ports=ports)
         ov, orules, ost = X.run_oracle(feats, data, lens, rules, stride=64)
         f = G.Filter(feats, devices=[0], ipv4_capacity=1 << 16, qt_min_keys=1)

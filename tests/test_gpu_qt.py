@@ -497,8 +497,8 @@ def test_qt_hits_concentrated_in_few_log_partitions(G, stride):
     rules = X.RuleSet()
     rules.v4_keys = keys
     rules.v4_vals = np.full(len(keys), 2, np.uint64)
-    # (2^21 packets: as many as the index has slots, so the log runs)
-    data, lens = X.gen_workload(82, 3, 1 << 21, stride, v4=keys, dst_permille=700)
+    # (2^22 packets: twice as many as the index has slots, so the log runs)
+    data, lens = X.gen_workload(82, 3, 1 << 22, stride, v4=keys, dst_permille=700)
     run_both(G, "xdpfilt_dny_all", rules, data, lens, stride)
 
 
