@@ -1291,6 +1291,9 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 // load per lane (a wave load covers 256 entries: about a uniform slice, so
 // few of the LDS atomics' lanes idle).
 constexpr int LC_THREADS = 1024;
+#ifndef XFG_LC_U   /* slices a wave has in flight (A/B) */
+#define XFG_LC_U 8
+#endif
 
 __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kargs a, uint32_t hist_n)
 {
@@ -1299,7 +1302,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	// (partition p, pass j: local indices [j * hist_n, (j + 1) * hist_n))
 	const uint32_t tid = threadIdx.x, p = blockIdx.x % XFG_LOG_PARTS, lane = tid & 63, w = tid >> 6;
 	const uint32_t j0 = (blockIdx.x / XFG_LOG_PARTS) * hist_n;
-	constexpr uint32_t NWV = LC_THREADS / 64, U = 8, J = XFG_LOG_HIST_MAX / LC_THREADS;
+	constexpr uint32_t NWV = LC_THREADS / 64, U = XFG_LC_U, J = XFG_LOG_HIST_MAX / LC_THREADS;
 	// (S slices to read; PS between partitions: pending launches' logs side by side)
 	const uint32_t S = a.pcount, PS = a.pslices, cap = a.pcap;
 	// the identity span: hash-map + port counters, or the QT slots
@@ -1357,13 +1360,17 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	};
 	// (two rounds of U slices in flight: the next round's loads issued
 	// before this round's LDS atomics -- with the logs of several launches
-	// a wave takes dozens of slices)
+	// a wave takes dozens of slices; only the lanes whose 8 entries start
+	// inside the slice's fill load: at a quarter of the bench's batch a
+	// whole-wave load read four times the log, and the count kernel took
+	// 62 us for four launches' logs against 47, profiles/r05_s43_session.log)
 	auto ld = [&](uint32_t s0, u32x4 (&d)[U]) {
 #pragma unroll
 		for (uint32_t u = 0; u < U; u++) {
 			const uint32_t sl = s0 + u * NWV;
 			const u32x4 *e = (const u32x4 *)(base + (uint64_t)sl * cap);
-			d[u] = sl < S && s_fill[sl] ? __builtin_nontemporal_load(e + lane) : u32x4{ 0, 0, 0, 0 };
+			d[u] = sl < S && lane * 8 < s_fill[sl] ? __builtin_nontemporal_load(e + lane)
+							    : u32x4{ 0, 0, 0, 0 };
 		}
 	};
 	u32x4 v[U], nx[U];

@@ -30,11 +30,19 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # test that lowers the QT fold threshold),
 # XFG_LIB=asan the sanitizer build of the host C (the CPU suite under
 # tools/asan_suite.sh)
-# tools/ A/B runs may also name a library file outright (XFG_LIB=/path/x.so)
+# tools/ A/B runs may also name a library file outright (XFG_LIB=/path/x.so);
+# a named file that is missing, or an unknown name, is an error (never the
+# product library in its place)
 _LIBS = {"diag": ("lib", "libxdpfilter_gpu_diag.so"), "asan": ("lib-asan", "libxdpfilter_gpu.so")}
 _SEL = os.environ.get("XFG_LIB", "")
-LIB_PATH = (_SEL if _SEL.endswith(".so") and os.path.isfile(_SEL) else
-            os.path.join(os.path.dirname(HERE), *_LIBS.get(_SEL, ("lib", "libxdpfilter_gpu.so"))))
+if _SEL.endswith(".so"):
+    if not os.path.isfile(_SEL):
+        raise ImportError(f"XFG_LIB names {_SEL!r}, which does not exist")
+    LIB_PATH = _SEL
+elif _SEL and _SEL not in _LIBS:
+    raise ImportError(f"XFG_LIB={_SEL!r}: expected 'diag', 'asan' or a path to a .so")
+else:
+    LIB_PATH = os.path.join(os.path.dirname(HERE), *_LIBS.get(_SEL, ("lib", "libxdpfilter_gpu.so")))
 
 FEAT_TCP, FEAT_UDP, FEAT_IPV6, FEAT_IPV4, FEAT_ETHERNET = 1, 2, 4, 8, 16
 FEAT_ALL = 31
