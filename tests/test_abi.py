@@ -32,6 +32,18 @@ def test_library_exports_every_declared_symbol(header, listed):
     assert declared <= set(G.EXPORTS) | set(G.IO_EXPORTS)
 
 
+@pytest.mark.parametrize("sel", ["/nonexistent/libxdpfilter_gpu.so", "product"])
+def test_a_library_selection_that_names_nothing_fails_loudly(sel):
+    """XFG_LIB naming a missing file or an unknown build is an error, never the
+    product library loaded in its place."""
+    import subprocess
+    import sys
+    pydir = os.path.dirname(G.__file__)
+    r = subprocess.run([sys.executable, "-c", "import xfgpu"], cwd=pydir, capture_output=True,
+                       text=True, env=dict(os.environ, XFG_LIB=sel), timeout=120)
+    assert r.returncode != 0 and "XFG_LIB" in r.stderr
+
+
 def test_native_library_is_the_in_tree_build():
     assert os.path.realpath(G.LIB_PATH).startswith(os.path.realpath(ROOT))
     with open("/proc/self/maps") as f:
