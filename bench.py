@@ -48,14 +48,14 @@ KERNEL_OF_PATH = {
 # tools/pmc_summary.py): per launch path, the file and the batch it was taken at
 # (round 5: the QT kernel with pending logs and the mask-free rings; a pass of an
 # older kernel would misstate this one's traffic)
-PMC_OF_PATH = {5: ("profiles/r05_c3_pmc_2p26.json", 1 << 26)}
+PMC_OF_PATH = {5: ("profiles/archive/r05_c3_pmc_2p26.json", 1 << 26)}
 
 
 def committed_traffic(path, n, stream_bytes):
     """HBM bytes per launch from the committed PMC passes of this path's
     kernel at this batch, or None when no such file matches.  gfx950's
     FETCH_SIZE tallies a wide coalesced read at half its bytes and a random
-    32/64-byte line at its bytes (profiles/r02_fetch_size_calibration.json),
+    32/64-byte line at its bytes (profiles/archive/r02_fetch_size_calibration.json),
     so the frame + length stream's other half is added back, not the whole
     figure doubled; WRITE_SIZE as read."""
     ent = PMC_OF_PATH.get(path)
@@ -240,6 +240,7 @@ def main():
                      "GBps_h2d": round(hdata.nbytes / hs / 1e9, 1),
                      "registered_Mpps": round(hn / hr / 1e6, 1),
                      "registered_GBps_h2d": round(hdata.nbytes / hr / 1e9, 1),
+                     "gather_threads": int(G.lib.xfg_host_threads()),
                      "note": "host-resident batch incl. H2D frames+lens and D2H verdicts "
                              "(xfg_classify_host: pinned staging copy by the device's pool; "
                              "registered: the kernels read the caller's mapped pages in place)"}

@@ -246,6 +246,11 @@ int xfg_classify_host(xfg_ctx *ctx, int dev, const struct xfg_batch *batch,
 int xfg_host_register(xfg_ctx *ctx, void *p, size_t bytes);
 int xfg_host_unregister(xfg_ctx *ctx, void *p);
 
+/* Threads of a device's host-path gather pool (1-16): the process's CPU set,
+ * or XFG_HOST_THREADS, or OMP_NUM_THREADS when above 1 (torchrun's default
+ * of 1 is not taken as the process's share).  Performance only. */
+int xfg_host_threads(void);
+
 /*
  * AF_XDP RX in host memory: the consumer side of an XDP socket's RX ring
  * (xsk_ring_cons__peek() / xsk_ring_cons__rx_desc() / xsk_ring_cons__release(),

@@ -148,3 +148,94 @@ def test_eth_table_follows_map_edits(G):
             rules.eth_keys = np.vstack([k, extra])
             rules.eth_vals = np.append(rules.eth_vals, np.full(len(extra), 2, np.uint64))
     f.close()
+
+
+M32 = 0xffffffff
+ETH_SEED = 0x5eed1234 ^ 0xbb67ae85     # xfg_open's default seed ^ the Ethernet map's
+
+
+def _fmix32(h):
+    h = h.astype(np.uint64)
+    h ^= h >> 16
+    h = (h * 0x85ebca6b) & M32
+    h ^= h >> 13
+    h = (h * 0xc2b2ae35) & M32
+    h ^= h >> 16
+    return h
+
+
+def eth_home(keys, slots):
+    """The LDS key table's home entry of each MAC (xfg_hash_eth & (slots - 1))."""
+    k = np.ascontiguousarray(keys, np.uint8).reshape(-1, 6)
+    lo = k[:, :4].copy().view("<u4").reshape(-1).astype(np.uint64)
+    hi = (k[:, 4].astype(np.uint64) | (k[:, 5].astype(np.uint64) << 8))
+    h = _fmix32(lo ^ np.uint64(ETH_SEED))
+    h = _fmix32(h ^ hi)
+    return (h & np.uint64(slots - 1)).astype(np.int64)
+
+
+def test_eth_table_long_probe_chains_and_the_513th_key(G):
+    """A full table (512 keys, 1024 entries) with 40 keys sharing one home
+    entry, so every lookup reads 40+ entries (ek_disp), then a 513th insert
+    (the map past the table: the generic pipelined kernel) and a delete
+    back to 512 (the table again): verdicts, every rule value and the stats
+    equal the restatement's at each step."""
+    feats = X.VARIANT_FEATURES["xdpfilt_alw_eth"]
+    cand = X.rand_keys(301, 200000, 6)
+    home = eth_home(cand, 1024)
+    h0 = np.bincount(home).argmax()
+    same = cand[home == h0][:40]
+    assert len(same) == 40
+    rest = cand[home != h0][:472]
+    rng = np.random.default_rng(302)
+    rules = X.RuleSet()
+    rules.eth_keys = np.vstack([same, rest])
+    rules.eth_vals = rng.choice(np.array([1, 2, 3], np.uint64), 512) | \
+        (rng.integers(0, 30, 512).astype(np.uint64) << 6)
+    data, lens = eth_frames(303, 120000, 64, rules)
+    d = data.reshape(-1, 64)
+    pick = rng.choice(len(d), len(d) // 5, replace=False)       # the colliding keys, often
+    d[pick, 0:6] = same[rng.integers(0, 40, len(pick))]
+    f = make_filter(G, "xdpfilt_alw_eth")
+    f.load_rules(rules)
+    cur = rules.prepared().copy()
+    extra = X.rand_keys(304, 1, 6)
+    for step, path in enumerate([6, 1, 6]):
+        if step == 1:          # the 513th key
+            f.update(G.MAP_ETHERNET, bytes(extra[0]), 3)
+            cur.eth_keys = np.vstack([cur.eth_keys, extra])
+            cur.eth_vals = np.append(cur.eth_vals, np.uint64(3))
+        elif step == 2:        # one colliding key deleted: 512 again
+            f.delete(G.MAP_ETHERNET, bytes(cur.eth_keys[3]))
+            keep = np.ones(len(cur.eth_keys), bool)
+            keep[3] = False
+            cur.eth_keys, cur.eth_vals = cur.eth_keys[keep], cur.eth_vals[keep]
+        v = f.run(data, lens, stride=64)
+        assert f.last_path() == path, (step, f.last_path())
+        ov, cur, ost = X.run_oracle(feats, data, np.minimum(lens, 64), cur, stride=64)
+        assert_same(v, gpu_values(f, G, cur), f.stats(), ov, cur, ost)
+        f.stats_reset()
+    f.close()
+
+
+@pytest.mark.parametrize("variant", ["xdpfilt_dny_all", "xdpfilt_alw_all"])
+@pytest.mark.parametrize("stride", [64, 1536])
+def test_eth_table_beside_ip_rules(G, variant, stride):
+    """A few MAC rules beside IPv4, IPv6 and port rules (dny_all / alw_all):
+    the generic pipelined kernel answers both Ethernet lookups from the LDS
+    key table (a hit ends the program before any IP lookup,
+    xdpfilt_prog.h:224-227) and the IP keys by its Bloom and bucket stages:
+    verdicts, every rule value and the stats equal the restatement's."""
+    rules, pool = X.random_rules(311 + stride, n4=20000, n6=2000, ne=12, nports=30)
+    n = 200000 if stride == 64 else 30000
+    data, lens = X.gen_fuzz(312 + stride, n, stride, rules, pool)
+    d = data.reshape(n, stride)
+    rng = np.random.default_rng(313)
+    k = rules.eth_keys
+    dst = rng.choice(n, n // 8, replace=False)
+    d[dst, 0:6] = k[rng.integers(0, len(k), len(dst))]
+    src = rng.choice(n, n // 8, replace=False)
+    d[src, 6:12] = k[rng.integers(0, len(k), len(src))]
+    ov = run_check(G, variant, rules, data, lens, stride, path=1,
+                   ipv4_capacity=1 << 15, ipv6_capacity=1 << 12, eth_capacity=64)
+    assert len(np.unique(ov)) == 3

@@ -545,6 +545,33 @@ def test_classify_host_registered_slices(G, stride, first):
     f.close()
 
 
+@pytest.mark.parametrize("shift", [8, 4])
+def test_classify_host_registered_unaligned(G, shift):
+    """A registered buffer whose batch does not start 16-byte aligned: the
+    zero-copy path (16-byte loads in place) needs aligned slots, so the
+    batch takes the staged path -- results equal to the restatement."""
+    n, stride = 200000, 64
+    rules, pool = X.random_rules(91 + shift, n4=300, n6=100, ne=20, nports=40)
+    data, lens = X.gen_fuzz(17 + shift, n, stride, rules, pool)
+    buf = np.zeros(n * stride + 64, np.uint8)
+    assert buf.ctypes.data % 16 == 0
+    sub = buf[shift:shift + n * stride]
+    sub[:] = data[:n * stride]
+    assert sub.ctypes.data % 16 != 0
+    feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    ov, _, ost = X.run_oracle(feats, data, lens, rules, stride=stride, nthreads=8)
+    f = G.Filter(feats, ndev=1)
+    f.load_rules(rules)
+    f.host_register(buf)
+    try:
+        v = f.classify_host(sub, lens.astype(np.uint16), stride=stride)
+    finally:
+        f.host_unregister(buf)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(f.stats(), ost)
+    f.close()
+
+
 def test_classify_host_registered_large_slots_many_frames(G):
     """Registered 1536-byte slots, 798k frames read in place (zero copy)
     (500 rules: the generic pipelined kernel) and IPv6 frames whose

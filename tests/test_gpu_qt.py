@@ -548,6 +548,60 @@ def test_qt_with_ipv6_rules(G, variant, stride, dirs6):
     assert len(np.unique(ov)) == 3
 
 
+@pytest.mark.parametrize("variant", ["xdpfilt_dny_all", "xdpfilt_alw_ip"])
+@pytest.mark.parametrize("shape", ["sym", "asym"])
+@pytest.mark.parametrize("dirs6", ["dst", "src", "both"])
+def test_qt_both_ipv4_directions_with_ipv6_rules(G, variant, shape, dirs6):
+    """IPv4 rules on both lookup directions (`xdp-filter ip -m src,dst`:
+    lookup_verdict_ipv4, dst then src, xdpfilt_prog.h:121-134) beside IPv6
+    dst, src or src,dst rules (lookup_verdict_ipv6, :152-165): the index
+    kernel's two-stage IPv4 lookup and its in-loop IPv6 lookups together.
+    A third of the IPv6 frames carry a ruled source, a quarter of the IPv4
+    frames a ruled source; tiles of IPv6 frames only (more than 16 a tile)."""
+    rng = np.random.default_rng(141)
+    rules, v4, ports = one_direction_rules(142, 20000, 3)
+    if shape == "asym":
+        f = rules.v4_vals & ~np.uint64(3)
+        rules.v4_vals = f | rng.integers(0, 4, len(v4)).astype(np.uint64)
+    v6 = X.rand_keys(143, 4000, 16)
+    rules.v6_keys = v6
+    if dirs6 == "both":
+        f6 = rng.choice(np.array([1, 2, 3], np.uint64), len(v6))
+    else:
+        f6 = np.full(len(v6), 2 if dirs6 == "dst" else 1, np.uint64)
+    f6[rng.random(len(v6)) < 0.1] |= 4
+    rules.v6_vals = f6 | (rng.integers(0, 50, len(v6)).astype(np.uint64) << 6)
+    d1, l1 = X.gen_workload(144, 3, 1 << 16, 64, v4=v4, v6=v6, ports=ports)
+    fr = d1.reshape(-1, 64)
+    ip4 = np.nonzero((fr[:, 12] == 8) & (fr[:, 13] == 0))[0][::4]
+    fr[ip4, 26:30] = v4[(np.arange(len(ip4)) * 7919) % len(v4)]
+    six = np.nonzero((fr[:, 12] == 0x86) & (fr[:, 13] == 0xdd))[0]
+    srcs = six[::3]
+    fr[srcs, 22:38] = v6[rng.integers(0, len(v6), len(srcs))]
+    d2, l2 = fuzz_at(145, 1 << 14, 64, rules, ports)
+    pick = six[np.arange(1 << 13) % len(six)]
+    d3, l3 = fr[pick].reshape(-1), l1[pick]
+    data, lens = np.concatenate([d1, d2, d3]), np.concatenate([l1, l2, l3])
+    ov = run_both(G, variant, rules, data, lens, 64, ipv6_capacity=1 << 13)
+    assert len(np.unique(ov)) == 3
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("dirs6", ["dst", "both"])
+def test_qt_both_ipv4_directions_ipv6_in_loop(dirs6):
+    """With both IPv4 directions live the IPv6 frames are looked up in the
+    index kernel's loop, not deferred to the whole-frame walk: a fresh
+    process on the diagnostics library leaves deferred packets unclassified
+    (XFG_DIAG_MASK=2048) and every IPv6 frame still carries the oracle's
+    verdict (tests/gpu_defer_worker.py)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, XFG_LIB="diag")
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gpu_defer_worker.py"), dirs6],
+                       capture_output=True, text=True, timeout=280, env=env)
+    assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
+
+
 def test_qt_not_taken_with_ethernet_rules_live(G):
     """An Ethernet rule is tested on every frame before its IP keys
     (xdpfilt_prog.h:187-196): the index kernel, which carries IPv4 keys only,

@@ -128,3 +128,61 @@ def test_wide_hit_log_9m_rules_2p25(G, v6):
         fr[six, 22:38] = v6k[np.arange(len(six)) * 7919 % len(v6k)]
     ov, _ = _check(G, rules, data, lens.astype(np.uint16), cap=n4, **kw)
     assert (ov == 2).sum() > n // 3
+
+
+@pytest.mark.timeout(600)
+def test_qt_counts_cross_2p32_packets_product(G):
+    """More than 2^32 packets through the quotient index on one device, on
+    the product library: a 2^26-packet batch whose every frame hits ONE
+    rule, classified 65 times back to back (4.36e9 packets, all on that
+    rule's 32-bit QT-order count, xfg_kargs.qt_hits).  The runtime must fold
+    the counts into the 64-bit canonical counters before they could wrap
+    (xfg_ctx.c qt_fold_queued, at the real 2^32 threshold): the rule's value
+    is its pre-existing hits plus 65 * 2^26 (CHECK_MAP adds 1 << 6 a hit,
+    xdpfilt_prog.h:60-61), the stats 65 passes.  The batch is a 2^16-frame
+    pattern repeated, so the oracle runs on the pattern."""
+    rng = np.random.default_rng(201)
+    v4 = X.rand_keys(202, 20000, 4)
+    hot = v4[17]
+    rules = X.RuleSet()
+    rules.v4_keys = v4
+    rules.v4_vals = np.full(len(v4), 2, np.uint64) | (rng.integers(0, 50, len(v4)).astype(np.uint64) << 6)
+    ports = np.array([53, 80], np.uint16)
+    for p in ports:
+        rules.ports[X.port_key(int(p))] = 2 | 4 | 8
+    m, reps_tile, launches = 1 << 16, 1 << 10, 65
+    pd, pl = X.gen_workload(203, 3, m, 64, v4=hot.reshape(1, 4), ports=ports, dst_permille=1000,
+                            bad_permille=0)
+    fr = pd.reshape(m, 64)
+    ip4 = (fr[:, 12] == 8) & (fr[:, 13] == 0)
+    first = int(np.nonzero(ip4)[0][0])
+    fr[~ip4] = fr[first]                       # every frame IPv4, dst = the hot rule
+    pl[~ip4] = pl[first]
+    feats = X.VARIANT_FEATURES["xdpfilt_dny_all"]
+    ov, orules, ost = X.run_oracle(feats, pd, pl, rules, stride=64, nthreads=_threads())
+    assert (ov == 2).all()                     # every frame hits (PASS under deny)
+    n = m * reps_tile
+    total = n * launches
+    assert total > 1 << 32
+    data = np.tile(pd, reps_tile)
+    lens = np.tile(pl.astype(np.uint16), reps_tile)
+    f = make_filter(G, "xdpfilt_dny_all", ipv4_capacity=1 << 16, qt_min_keys=1)
+    f.load_rules(rules)
+    d_data, d_lens, d_v = f.alloc(data.nbytes), f.alloc(lens.nbytes), f.alloc(n)
+    d_data.upload(data)
+    d_lens.upload(lens)
+    del data
+    f.classify_timed(d_data.ptr, d_lens.ptr, n, 64, d_v.ptr, launches, lens_u16=True)
+    assert f.last_path() == f.PATH_QT
+    v = d_v.download(np.zeros(n, np.uint8))
+    assert (v == 2).all()
+    six = np.uint64(6)
+    pre = rules.v4_vals >> six
+    per_pass = (orules.v4_vals >> six) - pre            # the pattern's hits per rule
+    want = ((pre + per_pass * np.uint64(reps_tile * launches)) << six) | (rules.v4_vals & np.uint64(63))
+    got = f.values_of(G.MAP_IPV4, rules.prepared().v4_keys)
+    np.testing.assert_array_equal(got, want)
+    hot_i = int(np.nonzero((rules.prepared().v4_keys == hot).all(axis=1))[0][0])
+    assert int(got[hot_i] >> six) - int(pre[hot_i]) == total
+    np.testing.assert_array_equal(f.stats(), ost * (reps_tile * launches))
+    f.close()

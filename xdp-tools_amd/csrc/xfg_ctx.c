@@ -83,8 +83,8 @@ struct xfg_dev {
 	 * 5 pipelined IPv4-key mode over the quotient index, 6 Ethernet-key]
 	 * [window 64, 128][dynamic LDS: none, direct counters, port nibble map,
 	 * both] */
-	int occ[7][2][8];   /* [..][dynamic LDS: + bit 2, the Bloom words (bl_lds),
-			     * kind 6: the LDS key table] */
+	int occ[7][2][16];  /* [..][dynamic LDS: + bit 2, the Bloom words (bl_lds);
+			     * + bit 3, the LDS Ethernet key table (xfg_kargs.ek)] */
 	/* the Ethernet-key kernel's key table (kind 6), uploaded from ctx->ek
 	 * when ek_gen falls behind ctx->ek_gen; params read at launch under
 	 * d->lock */
@@ -265,10 +265,13 @@ static int keylen_of(int map)
 /* ------------------------------------------------------------------ gather pool */
 /* Persistent worker threads of one device's host path: hpool_run(fn, arg)
  * runs fn(arg, slice, nslices) for every slice, slice 0 on the caller.  As
- * many as the process's CPU set allows, capped by OMP_NUM_THREADS when set
- * (a shared box's CPU share: its CPU set shows the whole machine) and by
- * HOST_THREADS (performance only: the slices' results do not depend on
- * their count). */
+ * many as the process's CPU set allows, capped by HOST_THREADS; the
+ * caller's share of a shared box (whose CPU set shows the whole machine) is
+ * XFG_HOST_THREADS, else OMP_NUM_THREADS when it is above 1 -- a value of 1
+ * is what torch.distributed.run exports to every rank by default, and taken
+ * at its word it would leave each rank's gather one thread.  Performance
+ * only: the slices' results do not depend on their count.  xfg_host_threads()
+ * reports the size. */
 #define HOST_THREADS 16
 
 static int hpool_size(void)
@@ -277,15 +280,18 @@ static int hpool_size(void)
 	cpu_set_t cs;
 	if (!sched_getaffinity(0, sizeof(cs), &cs) && CPU_COUNT(&cs) > 0 && CPU_COUNT(&cs) < n)
 		n = CPU_COUNT(&cs);
+	const char *ht = getenv("XFG_HOST_THREADS");
 	const char *omp = getenv("OMP_NUM_THREADS");
-	if (omp && atoi(omp) > 0 && atoi(omp) < n)
+	if (ht && atoi(ht) > 0)
+		n = atoi(ht) < HOST_THREADS ? atoi(ht) : HOST_THREADS;
+	else if (omp && atoi(omp) > 1 && atoi(omp) < n)
 		n = atoi(omp);
-#ifdef XFG_DIAG
-	const char *ht = getenv("XFG_HOST_THREADS");   /* gather threads (round 4: 8) */
-	if (ht && atoi(ht) > 0 && atoi(ht) <= HOST_THREADS)
-		n = atoi(ht);
-#endif
 	return n;
+}
+
+int xfg_host_threads(void)
+{
+	return hpool_size();
 }
 
 struct hpool {
@@ -501,11 +507,11 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 
 	for (int k = 0; k < 7; k++)
 		for (int w = 0; w < 2; w++)
-			for (int c = 0; c < 8; c++)
+			for (int c = 0; c < 16; c++)
 				d->occ[k][w][c] = xfg_classify_occupancy(
 					ctx->prog_features, k, w ? 128 : 64,
 					(c & 1 ? XFG_DCNT_MAX * 4 : 0) + (c & 2 ? XFG_PORT_NIB_WORDS * 4 : 0) +
-					(c & 4 ? (k == 6 ? XFG_EK_SLOTS_MAX * 16 : XFG_BLOOM_LDS_MAX * 4) : 0));
+					(c & 4 ? XFG_BLOOM_LDS_MAX * 4 : 0) + (c & 8 ? 12 + XFG_EK_SLOTS_MAX * 16 : 0));
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -1616,8 +1622,11 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	/* the Ethernet-key kernel (kind 6): the Ethernet-only programs, their
 	 * map as an LDS key table -- every lookup answered in LDS, no frame
 	 * byte past the two addresses read */
-	int ek = a->pipe && (ctx->prog_features & XFG_FEAT_ETHERNET) &&
-		 !(ctx->prog_features & (XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_TCP | XFG_FEAT_UDP));
+	/* (and, since round 6, for the generic pipelined kernel -- live
+	 * Ethernet keys beside IP keys: dny_all / alw_all with a few MAC rules --
+	 * which answers both Ethernet lookups from the same table in LDS) */
+	const int ek_only = !(ctx->prog_features & (XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_TCP | XFG_FEAT_UDP));
+	int ek = a->pipe && (ctx->prog_features & XFG_FEAT_ETHERNET) && (ek_only || eth_live);
 #ifdef XFG_DIAG
 	const char *eo = getenv("XFG_EK");   /* "off": the generic pipelined kernel */
 	if (eo && !strcmp(eo, "off"))
@@ -1690,7 +1699,10 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * through a handful of overfull partitions to contended atomics) */
 	const uint64_t nkeys = (uint64_t)a.t4.count + a.t6.count + a.te.count;
 	const int logged = nkeys > XFG_LOG_MIN_KEYS;
-	const int log_no = !a.pipe || !logged || a.dcnt >= a.gbase[3] || a.ek || (cm && !strcmp(cm, "atomic"));
+	/* (the Ethernet-key kernel -- the Ethernet-only programs -- counts in LDS;
+	 * the generic kernel with the LDS key table logs its IP hits as usual) */
+	const int ek_only = a.pipe && a.ek && !(ctx->prog_features & (XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_TCP | XFG_FEAT_UDP));
+	const int log_no = !a.pipe || !logged || a.dcnt >= a.gbase[3] || ek_only || (cm && !strcmp(cm, "atomic"));
 	/* (a batch of fewer packets than counters: the count kernel's pass over
 	 * every counter costs more than the atomics it saves -- C5's 15M + 1M
 	 * rules at 2^23 packets: 0.45 ms with atomics, 0.65-0.71 with the log;
@@ -1714,7 +1726,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		/* (the log from twice as many packets as QT slots: at as many, C3's
 		 * and C4's 1M rules at 2^21 packets ran 0.068 / 0.088 ms with it and
 		 * 0.060 / 0.080 without; at twice, the same; at four times, the log
-		 * 10 % faster -- profiles/r05_s39_session.log) */
+		 * 10 % faster -- profiles/archive/r05_s39_session.log) */
 	}
 	const int log_off = log_no || nolog ||
 			    (!a.qt && (uint64_t)a.gbase[3] + XFG_PORT_MAP_ENTRIES > a.n);
@@ -1731,12 +1743,13 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.ek_slots = d->ek_slots;
 		a.ek_disp = d->ek_disp;
 	}
-	if (a.pipe && !a.km && !a.ek) {
+	if (a.pipe && !a.km && !ek_only) {
 		const struct xfg_tdesc *tt[3] = { &a.t4, &a.te, &a.t6 };
 		uint32_t tot = 0;
 		for (int i = 0; i < 3; i++) {
 			a.bl_off[i] = ~0u;
-			if (tt[i]->count && tt[i]->bloom_words) {
+			/* (the LDS key table answers the Ethernet lookups) */
+			if (tt[i]->count && tt[i]->bloom_words && !(i == 1 && a.ek)) {
 				a.bl_off[i] = tot;
 				tot += tt[i]->bloom_words;
 			}
@@ -1749,7 +1762,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			a.bl_lds = 0;
 #endif
 	}
-	const int kind = a.ek ? 6 : a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
+	const int kind = ek_only ? 6 : a.pipe ? (a.km ? (a.split ? 3 : (a.qt ? 5 : 2)) : 1) : 0, wi = a.window > 64;
 	if (a.qt) {   /* the index in stream order at this launch */
 		a.qt = d->qt_img;
 		a.qt_trans = d->qt_trans;
@@ -1772,7 +1785,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.qt_hits = d->qt_hits;
 	}
 	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) |
-				     (a.bl_lds || a.ek ? 4 : 0)];
+				     (a.bl_lds ? 4 : 0) | (a.ek ? 8 : 0)];
 #ifdef XFG_DIAG
 	const char *g = getenv("XFG_GRID_PER_CU");
 	if (g && *g)
@@ -1802,7 +1815,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.rec_port = d->rec + a.n;
 		a.rec_kb = both ? d->rec + 2 * a.n : NULL;
 	}
-	if (a.pipe && !a.ek) {   /* (the Ethernet-key kernel defers nothing) */
+	if (a.pipe && !ek_only) {   /* (the Ethernet-key kernel defers nothing) */
 		/* one deferred list per wave, room for every packet of its tiles */
 		uint64_t nw = grid * (per_wg / 64), nt = (a.n + 63) / 64;
 		uint64_t cap = (nt + nw - 1) / nw * 64;
@@ -1890,9 +1903,9 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	}
 	/* IPv6 rules beside the index: their lookups in the kernel's loop (1:
 	 * one IPv6 direction can hit, one line a frame; 2: both, the src line
-	 * beside the dst one), with one IPv4 direction live -- with both, every
-	 * IPv6 frame is deferred */
-	a.v6p = !(a.qt && a.v6d && d->qt_live != 3) ? 0u
+	 * beside the dst one), beside one live IPv4 direction or both (the
+	 * index never takes both directions with the u32 log: qt_log_fits) */
+	a.v6p = !(a.qt && a.v6d) ? 0u
 		: (a.t6.fmask & 3) == 3u ? 2u : (a.t6.fmask & 3) != 0 ? 1u : 0u;
 #ifdef XFG_DIAG
 	const char *v6e = getenv("XFG_V6P");   /* "off": every IPv6 frame deferred */
@@ -1913,7 +1926,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	/* classify, then its hit log's count kernel, on the device stream (a
 	 * count kernel on a second stream, overlapped with the next classify,
 	 * shares the CUs and slowed the classify more than it hid:
-	 * profiles/r04_s11_count_overlap.log) */
+	 * profiles/archive/r04_s11_count_overlap.log) */
 	uint64_t fold_at = 0xffffffffull;   /* (a 32-bit QT-order count's room) */
 #ifdef XFG_DIAG
 	const char *fa = getenv("XFG_QT_FOLD_AT");   /* tests: fold after this many packets */
@@ -2505,10 +2518,14 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 	 * copy: the kernel's loads cross PCIe, the window and whatever a
 	 * program walks past it, nothing else; whole frames in view, so no
 	 * fallback) -- the pool gathers the lengths only.  Measured on MI355X
-	 * against one DMA of the whole slots per chunk (C3, 64-byte frames):
-	 * 50 GB/s of frames against 34 (tools/zerocopy_probe.py). */
+	 * against one DMA of the whole slots per chunk (C3, 64-byte frames,
+	 * bench.py's host_path): 41-46 GB/s of frames against 34-36 on this
+	 * round's boxes (profiles/archive/r05_s16..s19, s36, s47).  The
+	 * slots must start 16-byte aligned, as the device path's batches do
+	 * (check_batch): an unaligned registered batch takes the staged path. */
 	const uint8_t *rbase = NULL;
 	int zc = (!src->descs && !src->offsets && src->stride && !(src->stride & 15) &&
+		  !((uintptr_t)src->data & 15) &&
 		  host_registered(ctx, src->data, n * (uint64_t)src->stride, &rbase)) ||
 		 /* AF_XDP frames in a registered UMEM: the descriptors' offsets
 		  * and lengths gathered, the frames read in place */

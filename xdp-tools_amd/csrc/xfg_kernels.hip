@@ -1323,8 +1323,10 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 		hist[i] = 0;
 #ifdef XFG_DIAG
 	const bool normw = (a.diag & 8192) != 0;   // (diagnostics: no counter read-modify-write)
+	// (diagnostics: 65536 the slices loaded but not added, 131072 no slice read)
+	const bool noadd = (a.diag & 65536) != 0, noslice = (a.diag & 131072) != 0;
 #else
-	constexpr bool normw = false;
+	constexpr bool normw = false, noadd = false, noslice = false;
 #endif
 #pragma unroll
 	for (uint32_t j = 0; j < J; j++)
@@ -1349,6 +1351,10 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	// uniform slice at the bench's batch; pcap is a multiple of 8, so every
 	// slice starts 16-byte aligned; the buffer has 512 entries of slack)
 	auto add8 = [&](u32x4 v, uint32_t i0, uint32_t np) {
+		if (noadd) {
+			asm volatile("" ::"v"(v));
+			return;
+		}
 #pragma unroll
 		for (uint32_t c = 0; c < 4; c++) {
 			const uint32_t l0 = (v[c] & 0xffff) - j0, l1 = (v[c] >> 16) - j0;
@@ -1363,7 +1369,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 	// a wave takes dozens of slices; only the lanes whose 8 entries start
 	// inside the slice's fill load: at a quarter of the bench's batch a
 	// whole-wave load read four times the log, and the count kernel took
-	// 62 us for four launches' logs against 47, profiles/r05_s43_session.log)
+	// 62 us for four launches' logs against 47, profiles/archive/r05_s43_session.log)
 	auto ld = [&](uint32_t s0, u32x4 (&d)[U]) {
 #pragma unroll
 		for (uint32_t u = 0; u < U; u++) {
@@ -1374,9 +1380,9 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 		}
 	};
 	u32x4 v[U], nx[U];
-	if (!a.pwide && w < S)
+	if (!a.pwide && w < S && !noslice)
 		ld(w, v);
-	for (uint32_t s0 = a.pwide ? S : w; s0 < S; s0 += NWV * U) {
+	for (uint32_t s0 = a.pwide || noslice ? S : w; s0 < S; s0 += NWV * U) {
 		if (s0 + NWV * U < S)
 			ld(s0 + NWV * U, nx);
 #pragma unroll
@@ -1537,13 +1543,18 @@ void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 
 // (qt_live 3: both IPv4 lookups through the index; pwide: an index past
 // 2^20 buckets, one lookup direction -- the host takes no other; v6p: the
-// IPv6 lookups in the loop, 1 one direction, 2 both, with one IPv4 direction)
+// IPv6 lookups in the loop, 1 one direction, 2 both, beside one IPv4
+// direction or both)
 template <uint32_t FEAT, bool L16>
 void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
 	if constexpr ((FEAT & F_IPV6) != 0)
 		if (a.v6p) {
-			if (a.v6p == 2 && a.pwide)
+			if (a.qt_live == 3 && a.v6p == 2)
+				launch_pipeq2<FEAT, L16, true, false, 2>(a, grid, dl, s);
+			else if (a.qt_live == 3)
+				launch_pipeq2<FEAT, L16, true, false, 1>(a, grid, dl, s);
+			else if (a.v6p == 2 && a.pwide)
 				launch_pipeq2<FEAT, L16, false, true, 2>(a, grid, dl, s);
 			else if (a.v6p == 2)
 				launch_pipeq2<FEAT, L16, false, false, 2>(a, grid, dl, s);
@@ -1738,6 +1749,7 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 				if constexpr ((FEAT & F_IPV6) != 0) {
 					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, false, 1>, QT_THREADS(64));
 					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, true, 2>, QT_THREADS(64));
+					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, true, false, 2>, QT_THREADS(64));
 				}
 			} else {
 				q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, false, 0>, QT_THREADS(128));
@@ -1746,6 +1758,7 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 				if constexpr ((FEAT & F_IPV6) != 0) {
 					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, false, 1>, QT_THREADS(128));
 					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, true, 2>, QT_THREADS(128));
+					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, true, false, 2>, QT_THREADS(128));
 				}
 			}
 			n = m;

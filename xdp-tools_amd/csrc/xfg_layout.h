@@ -54,7 +54,7 @@
  * indexed: any other key cannot hit this lookup, exactly as an absent one.
  * QT slot bucket * 16 + entry maps back to the canonical slot through
  * trans[] (the count kernel's job).  What a tile's lookups cost is set by
- * the random LINES they touch (tools/mb_vm.hip, profiles/r03_mb_vm*.log:
+ * the random LINES they touch (tools/mb_vm.hip, profiles/archive/r03_mb_vm*.log:
  * 64 lines per 64-packet tile add ~0.25 ms per 2^26 packets to the frame
  * stream, 32 lines 0.07, 16 lines 0.02; a table of 0.5-4 MB the same), so
  * a bucket is one line's worth, and 16 entries at < 8 keys per bucket

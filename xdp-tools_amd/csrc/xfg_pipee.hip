@@ -17,7 +17,7 @@
 // own bytes and no deferred packet.  The generic pipelined kernel
 // (xfg_pipeline.hip) spends ~380 vector instructions per 64-packet tile on
 // its general parse and plan for the same programs (C1 at 2^24: 6.0 per
-// packet, profiles/r05_s20_session.log).
+// packet, profiles/archive/r05_s20_session.log).
 //
 // A wave takes G tiles of 64 packets per iteration (one packet per lane per
 // tile; tiles dealt over the grid's waves as in the other pipelined kernels,
@@ -25,7 +25,7 @@
 // D - 1 iterations ahead into a ring of D register buffers.
 namespace {
 
-// (C1, one box, profiles/r05_s22_session.log and r05_s23_session.log: G 1
+// (C1, one box, profiles/archive/r05_s22_session.log and r05_s23_session.log: G 1
 // and D 2 0.185 ms at 2^24; G 2 0.190-0.201, G 4 0.209, G 8 0.258; D 3 and
 // 4 and 8 waves a SIMD slower -- the smaller loop body wins)
 #ifndef XFG_EK_G   /* tiles per wave iteration */
@@ -39,12 +39,6 @@ namespace {
 #ifndef XFG_EK_MINW   /* waves per SIMD the register budget allows for */
 #define XFG_EK_MINW 6
 #endif
-
-// The key table in LDS: 16-byte aligned, past the direct counters.
-__device__ __forceinline__ u32x4 *ek_base(const xfg_kargs &a, uint32_t *s_dyn)
-{
-	return reinterpret_cast<u32x4 *>(dcnt_base(a, s_dyn) + ((a.dcnt + 3) & ~3u));
-}
 
 template <uint32_t FEAT, bool L16>
 __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(const xfg_kargs a)
@@ -104,17 +98,7 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 	// its home (a key sits at most that far past it; keys are unique, so at
 	// most one entry matches).
 	auto probe = [&](uint32_t lo, uint32_t hi, uint32_t mask, uint32_t &slot) {
-		const uint32_t h = xfg_hash_eth(lo | ((uint64_t)hi << 32), seed);
-		uint32_t e = h & (es - 1);
-		bool hit = false;
-		for (uint32_t d = 0; d <= edisp; d++) {
-			const u32x4 v = s_ek[e];
-			const bool m = (v.x == lo) & (v.y == hi) & ((v.w & XFG_EK_VALID) != 0);
-			hit |= m & ((v.w & mask) == mask);
-			slot = m ? v.z : slot;
-			e = (e + 1) & (es - 1);
-		}
-		return hit;
+		return ek_probe(s_ek, es, edisp, seed, lo, hi, mask, slot);
 	};
 
 	// a group's first 16 bytes and lengths (tiles past the wave's share and

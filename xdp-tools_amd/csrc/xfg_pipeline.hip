@@ -53,7 +53,7 @@ constexpr uint32_t A_DEFER = 6;
 // the quotient-index kernel (xfg_pipeq.hip): waves per workgroup (two
 // workgroups per CU).  10 (5 waves per SIMD, 96 VGPRs) sped the stream and
 // parse up 4 % but the whole classify down 4 %: more requests in flight
-// than the CU's vector memory path serves (profiles/r03_qt_waves_ab.log)
+// than the CU's vector memory path serves (profiles/archive/r03_qt_waves_ab.log)
 #ifndef XFG_QT_NW
 #define XFG_QT_NW 8
 #endif
@@ -122,9 +122,37 @@ __device__ __forceinline__ u32x4 gload128(uint64_t addr)
 // folded into one load through a select of field addresses, which moves the
 // whole argument struct to scratch memory.
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
 __device__ __forceinline__ uint64_t rfl64(uint64_t x)
 {
 	return ((uint64_t)rfl((uint32_t)(x >> 32)) << 32) | rfl((uint32_t)x);
+}
+
+// The key table in LDS: 16-byte aligned, past the direct counters and the
+// staged Bloom words (the generic pipelined kernel's; none here).
+__device__ __forceinline__ u32x4 *ek_base(const xfg_kargs &a, uint32_t *s_dyn)
+{
+	return reinterpret_cast<u32x4 *>(dcnt_base(a, s_dyn) + ((a.dcnt + a.bl_lds + 3) & ~3u));
+}
+
+// CHECK_MAP (xdpfilt_prog.h:56-64) of one MAC against the LDS key table
+// (es entries, keys at most edisp past their home): found with every bit of
+// mask set; its canonical slot.  Every lane reads edisp + 1 entries (keys
+// are unique: at most one matches).
+__device__ __forceinline__ bool ek_probe(const u32x4 *s_ek, uint32_t es, uint32_t edisp, uint32_t seed,
+					 uint32_t lo, uint32_t hi, uint32_t mask, uint32_t &slot)
+{
+	const uint32_t h = xfg_hash_eth(lo | ((uint64_t)hi << 32), seed);
+	uint32_t e = h & (es - 1);
+	bool hit = false;
+	for (uint32_t d = 0; d <= edisp; d++) {
+		const u32x4 v = s_ek[e];
+		const bool m = (v.x == lo) & (v.y == hi) & ((v.w & XFG_EK_VALID) != 0);
+		hit |= m & ((v.w & mask) == mask);
+		slot = m ? v.z : slot;
+		e = (e + 1) & (es - 1);
+	}
+	return hit;
 }
 
 template <int KM>
@@ -309,9 +337,18 @@ __device__ __forceinline__ bool parse_static(const uint32_t *row, uint32_t len, 
 // when every one of them misses: ABORTED at a failed header check, else the
 // port stage (lookup_verdict_tcp/udp, :76-101, answered from LDS) or MISS.
 // Key mode 1 keeps only the IPv4 stage.
+// (ek.on: the Ethernet map as the LDS key table of a small map,
+// xfg_kargs.ek -- both Ethernet lookups answered here, exactly, and a hit
+// ends the program, :224-227; no Bloom word, no bucket line)
+struct EkL {
+	const u32x4 *tab;
+	uint32_t es, disp, seed, gb;
+	bool on;
+};
+
 template <uint32_t FEAT, int W, int KM, int PK>
 __device__ __forceinline__ void plan_packet(const xfg_kargs &a, const PktL<W> &p, const Parsed &r,
-					    const uint32_t *s_ports, uint32_t (&kd)[PK],
+					    const uint32_t *s_ports, const EkL &ek, uint32_t (&kd)[PK],
 					    uint32_t (&kh)[PK], uint32_t (&kv)[PK], uint32_t &nk,
 					    uint32_t &fb_act, uint32_t &fb_tag, bool &over)
 {
@@ -349,7 +386,23 @@ __device__ __forceinline__ void plan_packet(const xfg_kargs &a, const PktL<W> &p
 	}
 	if constexpr ((FEAT & F_ETH) != 0 && KM == 0) {
 		// lookup_verdict_ethernet: dst then src (xdpfilt_prog.h:187-196)
-		if (a.te.count) {
+		if (a.te.count && ek.on) {
+			uint32_t w0, w1, w2, w3, sl = 0;
+			bool h = false;
+			if (can_hit(a.te.fmask, M_DST)) {
+				key_words(p, K_ETH, 0, w0, w1, w2, w3);
+				h = ek_probe(ek.tab, ek.es, ek.disp, ek.seed, w0, w1, M_DST, sl);
+			}
+			if (!h && can_hit(a.te.fmask, M_SRC)) {
+				key_words(p, K_ETH, 6, w0, w1, w2, w3);
+				h = ek_probe(ek.tab, ek.es, ek.disp, ek.seed, w0, w1, M_SRC, sl);
+			}
+			if (h) {
+				fb_act = (FEAT & F_DENY) ? A_PASS : A_DROP;
+				fb_tag = ek.gb + sl;
+				return;
+			}
+		} else if (a.te.count) {
 			if (can_hit(a.te.fmask, M_DST))
 				add(K_ETH, M_DST, 0, 0);
 			if (can_hit(a.te.fmask, M_SRC))
@@ -437,6 +490,21 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 				s_bl[T.blo[i] + w] = src[w];
 		}
 	}
+	// (ek: a small Ethernet map as its LDS key table, past the Bloom words;
+	// its hits count in the LDS counter cache, as the Ethernet-key kernel's)
+	EkL ek{ ek_base(a, s_dyn), 0, 0, 0, 0, false };
+	if constexpr ((FEAT & F_ETH) != 0 && KM == 0) {
+		if (a.ek) {
+			ek.es = rfl(a.ek_slots);
+			ek.disp = rfl(a.ek_disp);
+			ek.seed = rfl(a.te.seed);
+			ek.gb = rfl(a.gbase[2]);
+			ek.on = true;
+			u32x4 *const s_ek = const_cast<u32x4 *>(ek.tab);
+			for (uint32_t i = tid; i < ek.es; i += NT)
+				s_ek[i] = reinterpret_cast<const u32x4 *>(a.ek)[i];
+		}
+	}
 	__syncthreads();
 
 	uint32_t *const rows = win + wv * 64 * ROWDW;
@@ -449,8 +517,9 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 	// a hit goes to the hit log when there is one and its counter is a
 	// hash-map slot without a direct LDS counter; else to the Counters
 	const uint32_t lg_lo = a.dcnt, lg_hi = a.tlog ? a.gbase[3] : 0u;
+	const uint32_t lg_eth = ek.on ? rfl(a.gbase[2]) : 0xffffffffu;   // (ek: Ethernet counters not logged)
 	auto count = [&](uint32_t tag) {
-		const bool lg = tag >= lg_lo && tag < lg_hi;
+		const bool lg = tag >= lg_lo && tag < lg_hi && tag < lg_eth;
 		log_append(tregion, tn, lg ? tag : CT_NONE, lane);
 		cn.bump(a, lg ? CT_NONE : tag, lane);
 	};
@@ -653,7 +722,7 @@ __global__ __launch_bounds__(PIPE_THREADS(W), (W) <= 64 ? 4 : 2) void xfg_pipeli
 				bool over = false;
 				PktL<W> p{ myrow, len, false };
 				if (parse_static<FEAT, W>(myrow, len, r))
-					plan_packet<FEAT, W, KM, PK>(a, p, r, s_ports, q_kd, q_kh, q_kv, q_nk,
+					plan_packet<FEAT, W, KM, PK>(a, p, r, s_ports, ek, q_kd, q_kh, q_kv, q_nk,
 								     q_act, q_tag, over);
 				else
 					over = true;

@@ -9,7 +9,7 @@
 // gfx950 what a tile's random reads cost beside the frame stream is set by
 // the distinct LINES they touch: 64 random lines per 64-packet tile add
 // ~0.25 ms per 2^26 packets, 32 lines 0.07, 16 lines 0.02, from a table of
-// 0.5 to 4 MB alike (tools/mb_vm.hip, profiles/r03_mb_vm*.log).  The
+// 0.5 to 4 MB alike (tools/mb_vm.hip, profiles/archive/r03_mb_vm*.log).  The
 // quotient index is the IPv4 map reduced to one 32-byte bucket per lookup
 // -- 2^bits buckets of 16 entries, a bijective key hash so that a bucket's
 // 15-bit remainders identify their keys exactly, only keys that carry the
@@ -164,7 +164,11 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// only where the dst lookup decided nothing (lookup_verdict_ipv6,
 	// xdpfilt_prog.h:152-165: dst first, the first hit's counter alone)
 	constexpr bool V6P = V6 != 0, V6B = V6 == 2;
-	static_assert(V6 <= 2 && (!V6P || ((FEAT & F_IPV6) != 0 && !BOTH)), "IPv6 lookups: one IPv4 direction");
+	// (with both IPv4 directions (BOTH) the IPv6 frames' results ride in
+	// R2's state with every other frame's: their lookups are the R stage's,
+	// an IPv6 frame has no IPv4 src lookup to wait for)
+	static_assert(V6 <= 2 && (!V6P || ((FEAT & F_IPV6) != 0 && !WIDE) || !BOTH), "IPv6 lookups");
+	static_assert(V6 <= 2 && (!V6P || (FEAT & F_IPV6) != 0), "IPv6 lookups need the IPv6 feature");
 	// bucket loads per iteration issued before the windows (L, L6)
 	constexpr uint32_t NL = 2 + (SPEC ? 2 : 0) + (V6P ? 1 : 0) + (V6B ? 1 : 0);
 	static_assert(D == 2 || (D == 3 && LAG == 2), "window depth: 2, or 3 with a bucket lag of 2");

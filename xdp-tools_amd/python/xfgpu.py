@@ -61,7 +61,7 @@ EXPORTS = [
     "xfg_host_alloc_pinned", "xfg_host_free_pinned", "xfg_classify_timed", "xfg_stream_read_timed",
     "xfg_comm_unique_id", "xfg_comm_init", "xfg_comm_allreduce", "xfg_map_update_batch_percpu",
     "xfg_classify_descs", "xfg_compact", "xfg_classify_xsk_host", "xfg_host_register",
-    "xfg_host_unregister", "xfg_last_path",
+    "xfg_host_unregister", "xfg_last_path", "xfg_host_threads",
 ]
 # include/xdpfilter_io.h
 IO_EXPORTS = [
@@ -144,6 +144,7 @@ def _load():
         "xfg_classify_xsk_host": (C.c_int, [vp, C.c_int, C.POINTER(DescBatch), C.c_uint64, vp]),
         "xfg_host_register": (C.c_int, [vp, vp, C.c_size_t]),
         "xfg_host_unregister": (C.c_int, [vp, vp]),
+        "xfg_host_threads": (C.c_int, []),
         "xfg_compact": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
         "xfg_classify_timed": (C.c_int, [vp, C.c_int, C.POINTER(Batch), vp, C.c_int,
                                          C.POINTER(C.c_double)]),
