@@ -14,8 +14,8 @@ overflow (their misses and their spilled keys decided by the canonical
 table), rebuilds after inserts / deletes / flag changes between batches,
 both IPv4 directions live (one image for src|dst rule sets, two
 otherwise), single edits patched into the index between batches, IPv6
-rules beside the index (IPv6 frames deferred), and the hit log in one and
-in two count passes.  The kernel logs its hits only for batches of at least
+rules beside the index (their lookups in the kernel's loop, beside one or
+both IPv4 directions), and the hit log in one and in two count passes.  The kernel logs its hits only for batches of at least
 as many packets as the index has slots (xfg_ctx.c launch_batch); the
 smaller batches here count through its LDS counter cache and atomics.
 """

@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--log2-packets", type=int, default=22)
     ap.add_argument("--src-dst", action="store_true", help="every rule src|dst")
     ap.add_argument("--hot", type=int, default=0, help="every dst hit on one of N rules")
+    ap.add_argument("--reps", type=int, default=1,
+                    help="classify the batch N times back to back (the count wave counts each "
+                         "launch's log in the next): counters and stats N times the oracle's")
     a = ap.parse_args()
     import xfgpu as G
     n = 1 << a.log2_packets
@@ -40,14 +43,28 @@ def main():
     ov, orules, ost = X.run_oracle(feats, data, lens, rules, stride=64, nthreads=16)
     f = G.Filter(feats, ndev=1, ipv4_capacity=1_000_000)
     f.load_rules(rules)
-    v = f.run(data, lens.astype(np.uint16), stride=64)
+    if a.reps == 1:
+        v = f.run(data, lens.astype(np.uint16), stride=64)
+    else:
+        l16 = lens.astype(np.uint16)
+        d_data, d_lens, d_v = f.alloc(data.nbytes), f.alloc(l16.nbytes), f.alloc(n)
+        d_data.upload(data)
+        d_lens.upload(l16)
+        f.classify_timed(d_data.ptr, d_lens.ptr, n, 64, d_v.ptr, a.reps, lens_u16=True)
+        v = d_v.download(np.zeros(n, np.uint8))
+        six, r = np.uint64(6), np.uint64(a.reps)
+        pre = rules.v4_vals >> six
+        orules.v4_vals = ((pre + ((orules.v4_vals >> six) - pre) * r) << six) | (rules.v4_vals & np.uint64(63))
+        pp = rules.ports >> six
+        orules.ports = ((pp + ((orules.ports >> six) - pp) * r) << six) | (rules.ports & np.uint64(63))
+        ost = ost * a.reps
     path = f.last_path()
     from test_gpu import gpu_values
     got = gpu_values(f, G, rules)
     st = f.stats()
     ok = (np.array_equal(v, ov) and np.array_equal(got.v4_vals, orules.v4_vals)
           and np.array_equal(got.ports, orules.ports) and np.array_equal(st, ost))
-    print(f"ab_parity lib={os.environ.get('XFG_LIB')} path={path} n={n} hot={a.hot} "
+    print(f"ab_parity lib={os.environ.get('XFG_LIB')} path={path} n={n} hot={a.hot} reps={a.reps} "
           f"verdicts={'ok' if np.array_equal(v, ov) else 'DIFF'} "
           f"v4={'ok' if np.array_equal(got.v4_vals, orules.v4_vals) else 'DIFF'} "
           f"stats={'ok' if np.array_equal(st, ost) else 'DIFF'} -> {'PASS' if ok else 'FAIL'}",

@@ -1,0 +1,33 @@
+# GPU session 2 (round 6): the QT kernel's bucket match A/B: base (SDWA compares, masks in SGPRs) / pkm
+# (packed u16 min) / plip (pkm + the halves swapped in place) / cw (pkm +
+# the count wave: the previous launch's log counted inside the next
+# launch), parity first.
+R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out; mkdir -p $OUT; export PYTHONUNBUFFERED=1
+step() {
+	local t=$1; shift
+	timeout -k 10 "$t" "$@"
+	local rc=$?
+	if [ $rc -eq 124 ] || [ $rc -gt 128 ]; then echo "STOP: rc=$rc from: $*"; exit $rc; fi
+	return $rc
+}
+cd $R
+echo "== parity (A/B libraries)"
+for v in pkm plip cw; do
+	for args in "" "--src-dst" "--hot 8" "--log2-packets 24"; do
+		XFG_LIB=$R/tools/abl/$v.so step 300 python3 tools/ab_parity.py $args || exit 2
+	done
+done
+# (the count wave counts each launch's log in the next: several launches)
+for args in "--reps 5" "--reps 5 --src-dst" "--reps 4 --hot 8" "--reps 3 --log2-packets 24"; do
+	XFG_LIB=$R/tools/abl/cw.so step 300 python3 tools/ab_parity.py $args || exit 2
+done
+echo "== A/B timing"
+for lg in 26 24; do
+	for r in 1 2; do
+		for v in base pkm plip cw; do
+			XFG_LIB=$R/tools/abl/$v.so step 300 python3 tools/explore.py --log2-packets $lg --rounds 3 --iters 10 1000000:500:250 > $OUT/s2_ab_${v}_${lg}_$r.log 2>&1 || exit 3
+			sed "s/^/$v 2^$lg /" $OUT/s2_ab_${v}_${lg}_$r.log | grep scenario
+		done
+	done
+done
+echo s2 done

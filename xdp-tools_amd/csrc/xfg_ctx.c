@@ -83,8 +83,9 @@ struct xfg_dev {
 	 * 5 pipelined IPv4-key mode over the quotient index, 6 Ethernet-key]
 	 * [window 64, 128][dynamic LDS: none, direct counters, port nibble map,
 	 * both] */
-	int occ[7][2][16];  /* [..][dynamic LDS: + bit 2, the Bloom words (bl_lds);
-			     * + bit 3, the LDS Ethernet key table (xfg_kargs.ek)] */
+	int occ[8][2][16];  /* [..][dynamic LDS: + bit 2, the Bloom words (bl_lds);
+			     * + bit 3, the LDS Ethernet key table (xfg_kargs.ek)]; kind 7:
+			     * kind 5 with its count wave (0: cannot launch) */
 	/* the Ethernet-key kernel's key table (kind 6), uploaded from ctx->ek
 	 * when ek_gen falls behind ctx->ek_gen; params read at launch under
 	 * d->lock */
@@ -135,6 +136,10 @@ struct xfg_dev {
 	 * launch of another shape */
 	uint32_t log_pend, log_grid;
 	struct xfg_kargs log_args;
+	/* (log_cw: the pending log was written in the count wave's mode --
+	 * one launch's slices, set log_first of two -- for the next launch's
+	 * count wave to take; log_first: the first pending slice) */
+	uint32_t log_cw, log_first;
 	uint32_t *rec;                  /* split classify: parse-pass records */
 	uint64_t rec_bytes;
 	unsigned long long *cstatus;    /* verdict compaction: tile status words */
@@ -505,13 +510,14 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 	HIPCHK(hipEventCreateWithFlags(&d->ev_user, hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
 
-	for (int k = 0; k < 7; k++)
+	for (int k = 0; k < 8; k++)
 		for (int w = 0; w < 2; w++)
 			for (int c = 0; c < 16; c++)
 				d->occ[k][w][c] = xfg_classify_occupancy(
 					ctx->prog_features, k, w ? 128 : 64,
 					(c & 1 ? XFG_DCNT_MAX * 4 : 0) + (c & 2 ? XFG_PORT_NIB_WORDS * 4 : 0) +
-					(c & 4 ? XFG_BLOOM_LDS_MAX * 4 : 0) + (c & 8 ? 12 + XFG_EK_SLOTS_MAX * 16 : 0));
+					(c & 4 ? XFG_BLOOM_LDS_MAX * 4 : 0) + (c & 8 ? 12 + XFG_EK_SLOTS_MAX * 16 : 0) +
+					(k == 7 ? 16 + XFG_CW_HIST_MAX * 4 : 0));
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -678,10 +684,22 @@ static int log_flush_locked(struct xfg_dev *d)
 		return 0;
 	struct xfg_kargs c = d->log_args;
 	c.pcount = d->log_pend * d->log_grid;
+	c.pfirst = d->log_first;   /* (the count wave's mode: the set of the last launch) */
+	c.cw_n = 0;
 	d->log_pend = 0;
 	int err = hip_err(hipSetDevice(d->ordinal));
 	if (!err)
 		err = xfg_launch_log_count(&c, d->stream);
+	return err;
+}
+
+/* Both halves of the QT-order counts (the log's and the atomics',
+ * xfg_kargs.qt_hitx) into the canonical counters, one fold each. */
+static int qt_fold_launch(struct xfg_dev *d)
+{
+	int err = xfg_launch_qt_fold(d->qt_hits, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
+	if (!err)
+		err = xfg_launch_qt_fold(d->qt_hits + d->qt_n, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
 	return err;
 }
 
@@ -696,7 +714,7 @@ static int qt_fold_locked(struct xfg_dev *d)
 		return err;
 	err = hip_err(hipSetDevice(d->ordinal));
 	if (!err)
-		err = xfg_launch_qt_fold(d->qt_hits, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
+		err = qt_fold_launch(d);
 	if (!err)
 		err = hip_err(hipStreamSynchronize(d->stream));
 	if (!err) {
@@ -713,7 +731,7 @@ static int qt_fold_queued(struct xfg_dev *d)
 {
 	int err = log_flush_locked(d);
 	if (!err)
-		err = xfg_launch_qt_fold(d->qt_hits, d->qt_trans, d->m[0].hits, d->qt_n, d->stream);
+		err = qt_fold_launch(d);
 	if (!err)
 		d->qt_pk = 0;
 	return err;
@@ -1776,13 +1794,15 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.qt2 = d->qt_img + (uint64_t)a.qt_base * 2 / 4;
 		/* its QT-order counts (zeroed when (re)allocated; a resize only
 		 * follows a fold: qt_refresh) */
-		const uint64_t qb = (uint64_t)d->qt_n * 4, had = d->qt_hits_bytes;
+		/* (two halves: the log's counts, the atomics' -- xfg_kargs.qt_hitx) */
+		const uint64_t qb = (uint64_t)d->qt_n * 8, had = d->qt_hits_bytes;
 		if ((err = scratch(d, (void **)&d->qt_hits, &d->qt_hits_bytes, qb)))
 			goto out;
 		if (d->qt_hits_bytes != had &&
 		    (err = hip_err(hipMemsetAsync(d->qt_hits, 0, d->qt_hits_bytes, d->stream))))
 			goto out;
 		a.qt_hits = d->qt_hits;
+		a.qt_hitx = d->qt_hits + d->qt_n;
 	}
 	int per_cu = d->occ[kind][wi][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) |
 				     (a.bl_lds ? 4 : 0) | (a.ek ? 8 : 0)];
@@ -1841,6 +1861,17 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			a.defer_grid = (uint32_t)d->ncu * 2;
 		}
 	}
+	/* IPv6 rules beside the index: their lookups in the kernel's loop (1:
+	 * one IPv6 direction can hit, one line a frame; 2: both, the src line
+	 * beside the dst one), beside one live IPv4 direction or both (the
+	 * index never takes both directions with the u32 log: qt_log_fits) */
+	a.v6p = !(a.qt && a.v6d) ? 0u
+		: (a.t6.fmask & 3) == 3u ? 2u : (a.t6.fmask & 3) != 0 ? 1u : 0u;
+#ifdef XFG_DIAG
+	const char *v6e = getenv("XFG_V6P");   /* "off": every IPv6 frame deferred */
+	if (v6e && !strcmp(v6e, "off"))
+		a.v6p = 0;
+#endif
 	/* hit log (pipelined kernels): the hash-map counters without a direct
 	 * LDS counter, when the count kernel's histogram covers them; the wave
 	 * regions share the deferred lists' bound, the partition buffers hold
@@ -1872,12 +1903,30 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		while (K > 1 && K * grid > XFG_LOG_SLICES_MAX)
 			K--;
 	}
+	/* the count wave (since round 6): the quotient-index kernel's ninth wave
+	 * counts the previous launch's log while the others classify, so no
+	 * count kernel runs between launches -- two sets of slices used in
+	 * turn; for a 64-byte window, a u16 log in one histogram of at most
+	 * XFG_CW_HIST_MAX (C3's 1M rules: 8192), no IPv6 lookups in the loop,
+	 * and the kernel launchable with its histogram */
+	const int occ_c = (a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0);
+	int cw = logs && a.qt && !pwide && hist <= XFG_CW_HIST_MAX && a.window <= 64 && !a.v6p &&
+		 2 * grid <= XFG_LOG_SLICES_MAX && d->occ[7][0][occ_c] > 0;
+#ifdef XFG_DIAG
+	const char *cwe = getenv("XFG_CW");   /* "off": the count kernel every XFG_LOG_PEND launches */
+	if (cwe && !strcmp(cwe, "off"))
+		cw = 0;
+#endif
+	if (cw)
+		K = 2;
 	/* logs pending from earlier launches: counted first unless this one
-	 * appends to them (the same shape, the same counts) */
+	 * appends to them -- or, in the count wave's mode, counts them (the
+	 * same shape, the same counts) */
 	const int append = logs && K > 1 && d->log_pend && d->log_grid == grid &&
 			   d->log_args.pcap == pcap && d->log_args.pslices == K * grid &&
 			   d->log_args.log_span == hist && d->log_args.pwide == (uint32_t)pwide &&
-			   d->log_args.qt_hits == a.qt_hits && d->log_args.qt_n == a.qt_n;
+			   d->log_args.qt_hits == a.qt_hits && d->log_args.qt_n == a.qt_n &&
+			   d->log_cw == (uint32_t)cw;
 	if (d->log_pend && !append && (err = log_flush_locked(d)))
 		goto out;
 	if (logs) {
@@ -1901,17 +1950,6 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.log_span = (uint32_t)hist;
 		a.pwide = (uint32_t)pwide;
 	}
-	/* IPv6 rules beside the index: their lookups in the kernel's loop (1:
-	 * one IPv6 direction can hit, one line a frame; 2: both, the src line
-	 * beside the dst one), beside one live IPv4 direction or both (the
-	 * index never takes both directions with the u32 log: qt_log_fits) */
-	a.v6p = !(a.qt && a.v6d) ? 0u
-		: (a.t6.fmask & 3) == 3u ? 2u : (a.t6.fmask & 3) != 0 ? 1u : 0u;
-#ifdef XFG_DIAG
-	const char *v6e = getenv("XFG_V6P");   /* "off": every IPv6 frame deferred */
-	if (v6e && !strcmp(v6e, "off"))
-		a.v6p = 0;
-#endif
 	if (a.qt && !a.pbuf && !qt_nolog) {   /* (decided above: cannot happen) */
 		err = -EIO;
 		goto out;
@@ -1939,12 +1977,33 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 				break;
 			d->qt_pk += a.n;
 		}
-		if (a.pbuf && K > 1)
+		a.cw_n = 0;
+		a.pfirst = 0;
+		if (a.pbuf && cw) {
+			/* the pending launch's set, counted by this launch's count
+			 * wave (or, with none pending, none); this launch's log
+			 * into the other set */
+			if (d->log_pend) {
+				a.cw_n = (uint32_t)grid;
+				a.cw_s0 = d->log_first;
+			}
+			a.pslice0 = d->log_pend && !d->log_first ? (uint32_t)grid : 0u;
+		} else if (a.pbuf && K > 1) {
 			a.pslice0 = d->log_pend * (uint32_t)grid;
+		}
 		err = xfg_launch_classify(ctx->prog_features, &a, (unsigned)grid, d->stream);
-		if (!err && a.pbuf && K > 1) {
+		if (!err && a.pbuf && cw) {
 			d->log_args = a;
 			d->log_grid = (uint32_t)grid;
+			d->log_pend = 1;
+			d->log_first = a.pslice0;
+			d->log_cw = 1;
+		} else if (!err && a.pbuf && K > 1) {
+			if (!d->log_pend)
+				d->log_first = 0;
+			d->log_args = a;
+			d->log_grid = (uint32_t)grid;
+			d->log_cw = 0;
 			if (++d->log_pend == K)
 				err = log_flush_locked(d);
 		} else if (!err) {

@@ -850,7 +850,7 @@ struct Counters {
 		for (int i = tid; i < CC_ENTRIES; i += nthr)
 			if (ctag[i] != CT_NONE && ccnt[i]) {
 				if (ctag[i] & CT_QTAG)
-					gatomic_add32(a.qt_hits + (ctag[i] & ~CT_QTAG), ccnt[i]);
+					gatomic_add32(a.qt_hitx + (ctag[i] & ~CT_QTAG), ccnt[i]);
 				else
 					atomicAdd(global_counter(a, ctag[i]), (unsigned long long)ccnt[i]);
 			}
@@ -1318,7 +1318,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 		gid[j] = k < hist_n && l < a.log_span && g < total ? (a.qt_hits ? g : a.qt ? a.qt_trans[g] : g)
 								   : CT_NONE;
 	}
-	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * PS + tid] : 0u;
+	const uint32_t fl = tid < S ? a.pfill[(uint64_t)p * PS + a.pfirst + tid] : 0u;
 	for (uint32_t i = tid; i < hist_n; i += LC_THREADS)
 		hist[i] = 0;
 #ifdef XFG_DIAG
@@ -1336,7 +1336,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 		s_fill[tid] = min(fl, cap);
 	__syncthreads();
 	if (a.pwide) {   // (u32 local indices, a range beyond one pass)
-		const uint32_t *wb = reinterpret_cast<const uint32_t *>(a.pbuf) + (uint64_t)p * PS * cap;
+		const uint32_t *wb = reinterpret_cast<const uint32_t *>(a.pbuf) + ((uint64_t)p * PS + a.pfirst) * cap;
 		for (uint32_t sl = w; sl < S; sl += NWV) {
 			const uint32_t np = s_fill[sl];
 			for (uint32_t i = lane; i < np; i += 64) {
@@ -1346,7 +1346,7 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 			}
 		}
 	}
-	const uint16_t *base = a.pbuf + (uint64_t)p * PS * cap;
+	const uint16_t *base = a.pbuf + ((uint64_t)p * PS + a.pfirst) * cap;
 	// (a wave load covers 512 entries of a slice -- 16 bytes a lane: about a
 	// uniform slice at the bench's batch; pcap is a multiple of 8, so every
 	// slice starts 16-byte aligned; the buffer has 512 entries of slack)
@@ -1545,9 +1545,34 @@ void launch_pipeq2(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 // 2^20 buckets, one lookup direction -- the host takes no other; v6p: the
 // IPv6 lookups in the loop, 1 one direction, 2 both, beside one IPv4
 // direction or both)
+// (the count wave: a workgroup of nine waves, the histogram in dynamic LDS
+// past the direct counters; 64-byte windows, u16 logs, no IPv6 lookups in
+// the loop -- the host enables it for those launches only, xfg_ctx.c)
+template <uint32_t FEAT, bool L16, bool BOTH>
+void launch_pipeq_cw(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
+{
+	const size_t dlc = (size_t)((a.dcnt + 3) & ~3u) * 4 +
+			   (a.port_nib && !a.port_tab && a.port_count ? XFG_PORT_NIB_WORDS * 4 : 0) +
+			   (size_t)a.log_hist * 4;
+	(void)dl;
+	if (a.dense)
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, true, L16, BOTH, false, 0, true>), dim3(grid),
+				   dim3(QT_THREADS(64) + 64), dlc, s, a);
+	else
+		hipLaunchKernelGGL((xfg_pipeq_kernel<FEAT, 64, false, L16, BOTH, false, 0, true>), dim3(grid),
+				   dim3(QT_THREADS(64) + 64), dlc, s, a);
+}
+
 template <uint32_t FEAT, bool L16>
 void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
+	if (a.cw_n) {
+		if (a.qt_live == 3)
+			launch_pipeq_cw<FEAT, L16, true>(a, grid, dl, s);
+		else
+			launch_pipeq_cw<FEAT, L16, false>(a, grid, dl, s);
+		return;
+	}
 	if constexpr ((FEAT & F_IPV6) != 0)
 		if (a.v6p) {
 			if (a.qt_live == 3 && a.v6p == 2)
@@ -1698,16 +1723,44 @@ extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_karg
 	return e == hipSuccess ? 0 : -(int)e - 1000;
 }
 
+// Resident workgroups per CU of the quotient-index kernel with its count
+// wave, `dyn` bytes of dynamic LDS (the direct counters, the port map, the
+// histogram): 0 = it cannot launch (the host then counts with the count
+// kernel).  The fewest over the variants a launch may take.
+template <uint32_t FEAT>
+static int occupancy_cw(size_t dyn)
+{
+	int m = 0;
+	bool any = false;
+	if constexpr ((FEAT & F_IPV4) != 0) {
+		const void *k[4] = { (const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, false, 0, true>,
+				     (const void *)xfg_pipeq_kernel<FEAT, 64, false, false, false, false, 0, true>,
+				     (const void *)xfg_pipeq_kernel<FEAT, 64, true, true, true, false, 0, true>,
+				     (const void *)xfg_pipeq_kernel<FEAT, 64, false, false, true, false, 0, true> };
+		for (int i = 0; i < 4; i++) {
+			int x = 0;
+			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k[i], QT_THREADS(64) + 64, dyn) != hipSuccess)
+				return 0;
+			m = any ? (x < m ? x : m) : x;
+			any = true;
+		}
+	}
+	return m;
+}
+
 // Resident workgroups per CU of a classify kernel (persistent grid sizing)
 // with `dyn` bytes of dynamic LDS: kind 0 = general, 1 = pipelined (key
 // mode 0), 2 = pipelined (key mode 1), 5 = pipelined over the quotient
-// index, 6 = the Ethernet-key kernel; window 64 or 128.
+// index, 6 = the Ethernet-key kernel, 7 = kind 5 with its count wave (0:
+// it cannot launch); window 64 or 128.
 template <uint32_t FEAT>
 static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 {
 	int n = 0;
 	hipError_t e = hipSuccess;
 	bool done = false;
+	if (kind == 7)   // (the quotient-index kernel with its count wave, 64-byte windows)
+		return window <= 64 ? occupancy_cw<FEAT>(dyn) : 0;
 	if constexpr ((FEAT & F_IPV4) != 0) {
 #ifdef XFG_DIAG
 		if (kind == 3) {        // split: the lookup pass

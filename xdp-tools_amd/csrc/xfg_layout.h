@@ -101,6 +101,7 @@
 #define XFG_EK_VALID      0x100u  /* an occupied entry (beside the flag byte) */
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
 #define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
+#define XFG_CW_HIST_MAX   8192u   /* the QT kernel's count-wave histogram entries (32 KiB) */
 #define XFG_LOG_PASSES_MAX 32u    /* histogram passes per partition (span 512K) */
 #define XFG_LOG_SLICES_MAX 1024u  /* slices per partition: classify workgroups */
 #define XFG_DEFER_SRC_MAX 4096u   /* deferred lists (classify waves) xfg_defer_kernel takes */
@@ -198,9 +199,10 @@ struct xfg_kargs {
 	/* this launch's first slice of each partition (slices pslice0 ..
 	 * pslice0 + grid - 1: the quotient-index kernel's logs of up to
 	 * pslices / grid launches share the buffers, counted together) and
-	 * the count kernel's slices to read (0 .. pcount - 1) */
+	 * the count kernel's slices to read (pfirst .. pfirst + pcount - 1) */
 	uint32_t pslice0;
 	uint32_t pcount;
+	uint32_t pfirst;
 	uint32_t log_hist;
 	/* a partition's local-index range (log_span) beyond one histogram: the
 	 * count kernel takes it in passes of log_hist (one workgroup per
@@ -262,6 +264,20 @@ struct xfg_kargs {
 	uint32_t qt_base;
 	uint32_t qt_n;
 	uint32_t qt_live;
+	/* where the QT kernel's counts that bypass the hit log go -- a full
+	 * LDS ring, a chunk past its slice, the LDS counter cache's QT
+	 * entries, no log at all -- by atomics: the second half of the
+	 * allocation (qt_hits + qt_n), folded like the first, so that the
+	 * counts the log brings (the count kernel's, the count wave's) are
+	 * read-modify-writes no atomic races */
+	uint32_t *qt_hitx;
+	/* the count wave (the QT kernel's ninth wave, cw_n != 0): this
+	 * launch's workgroups count the previous launch's log -- its cw_n
+	 * slices from cw_s0 of every partition they own -- into qt_hits while
+	 * their other waves classify, hiding the count kernel; this launch's
+	 * own slices start at pslice0 (the other of two sets) */
+	uint32_t cw_n;
+	uint32_t cw_s0;
 };
 
 

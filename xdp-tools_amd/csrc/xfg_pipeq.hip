@@ -88,6 +88,12 @@
 #ifndef XFG_QT_CNT2      /* 1: the hit's ring atomics without exec masks (a word per lane past the rings) */
 #define XFG_QT_CNT2 1
 #endif
+#ifndef XFG_QT_PKM       /* 1: the bucket match by packed u16 min (no compare masks in SGPRs) */
+#define XFG_QT_PKM 1
+#endif
+#ifndef XFG_QT_PLIP      /* 1: the bucket halves swapped in place by inline asm */
+#define XFG_QT_PLIP 0
+#endif
 #ifndef XFG_QT_PADV      /* (A/B only: extra VALU / SALU instructions per tile, to price one) */
 #define XFG_QT_PADV 0
 #endif
@@ -119,8 +125,98 @@ __device__ __forceinline__ uint32_t qt_drain_one(const xfg_kargs &a, const uint3
 	return act;
 }
 
-template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE, uint32_t V6>
-__global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
+// The count wave (CW): the ninth wave of a quotient-index workgroup counts
+// the PREVIOUS launch's hit log while the other eight classify -- what the
+// count kernel does after a launch, hidden inside the next one.  For each
+// partition p this workgroup owns (p = blockIdx.x, + gridDim.x ...): the
+// cw_n slices from cw_s0 (u16 local indices, one pass: log_span ==
+// log_hist) summed in an LDS histogram, then added to p's QT-order counts
+// with plain read-modify-writes -- the partition's counts in qt_hits have no
+// other writer during the launch (the kernel's atomics go to qt_hitx).  A
+// load instruction covers 64 / G slices of G lanes, 8 entries a lane, G the
+// fewest lanes whose 8 G entries hold the partition's fullest slice (the
+// bench's 2^24 batch: ~115 entries a slice, four slices an instruction),
+// U instructions in flight.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+__device__ __noinline__ void qt_count_wave(const xfg_kargs &a, lds_u32 *hist)
+{
+	constexpr uint32_t U = 8;
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t S = rfl(a.cw_n), s0 = rfl(a.cw_s0), PS = rfl(a.pslices), cap = rfl(a.pcap);
+	const uint32_t hn = rfl(a.log_hist);
+	for (uint32_t p = blockIdx.x; p < XFG_LOG_PARTS; p += gridDim.x) {
+		for (uint32_t i = lane; i < hn; i += 64)
+			hist[i] = 0;
+		const uint32_t *pf = a.pfill + (uint64_t)p * PS + s0;
+		uint32_t mx = 0;
+		for (uint32_t s = lane; s < S; s += 64)
+			mx = max(mx, min(gld32(pf + s), cap));
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+		mx = rfl(mx);
+		const uint32_t lgG = mx <= 64 ? 3u : mx <= 128 ? 4u : mx <= 256 ? 5u : 6u;
+		const uint32_t G = 1u << lgG, per = 64u >> lgG;
+		const uint32_t lg = lane >> lgG, lr = lane & (G - 1);
+		const uint32_t chunks = (mx + G * 8 - 1) / (G * 8);   // (more than one: G 64 only)
+		const uint16_t *pb = a.pbuf + ((uint64_t)p * PS + s0) * cap;
+		__builtin_amdgcn_wave_barrier();
+		auto add8 = [&](const u32x4 &v, uint32_t i0, uint32_t f) {
+#pragma unroll
+			for (uint32_t c = 0; c < 4; c++) {
+				const uint32_t l0 = v[c] & 0xffffu, l1 = v[c] >> 16;
+				if (i0 + 2 * c < f && l0 < hn)
+					__atomic_fetch_add(&hist[l0], 1u, __ATOMIC_RELAXED);
+				if (i0 + 2 * c + 1 < f && l1 < hn)
+					__atomic_fetch_add(&hist[l1], 1u, __ATOMIC_RELAXED);
+			}
+		};
+		// work items: (slice group, chunk), U loads in flight
+		const uint32_t ngrp = (S + per - 1) / per, nitem = ngrp * chunks;
+		for (uint32_t it = 0; it < nitem; it += U) {
+			u32x4 v[U];
+			uint32_t fl[U], i0[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++) {
+				const uint32_t w = it + u, g = w / chunks, c = w - g * chunks;
+				const uint32_t sl = g * per + lg;
+				fl[u] = w < nitem && sl < S ? min(gld32(pf + sl), cap) : 0u;
+				i0[u] = c * G * 8 + lr * 8;
+				v[u] = i0[u] < fl[u] ? *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(
+								(uintptr_t)(pb + (uint64_t)sl * cap + i0[u]))
+						     : u32x4{ 0, 0, 0, 0 };
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				add8(v[u], i0[u], fl[u]);
+		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the histogram's atomics done
+		__builtin_amdgcn_wave_barrier();
+		// (R counts a lane loaded at once, then added and stored: the
+		// loads' latency paid once per R, not once per count)
+		constexpr uint32_t R = 16;
+		for (uint32_t l0 = 0; l0 < hn; l0 += 64 * R) {
+			uint32_t cur[R];
+#pragma unroll
+			for (uint32_t r = 0; r < R; r++) {
+				const uint32_t l = l0 + r * 64 + lane;
+				cur[r] = l < hn ? gld32(a.qt_hits + (((l >> 4) << 12) | (p << 4) | (l & 15))) : 0u;
+			}
+#pragma unroll
+			for (uint32_t r = 0; r < R; r++) {
+				const uint32_t l = l0 + r * 64 + lane;
+				const uint32_t c = l < hn ? (uint32_t)hist[l] : 0u;
+				if (c)
+					gst32(a.qt_hits + (((l >> 4) << 12) | (p << 4) | (l & 15)), cur[r] + c);
+			}
+		}
+		__builtin_amdgcn_wave_barrier();
+	}
+}
+
+template <uint32_t FEAT, int W, bool DENSE, bool L16, bool BOTH, bool WIDE, uint32_t V6, bool CW = false>
+__global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg_pipeq_kernel(const xfg_kargs a)
 {
 	static_assert((FEAT & F_IPV4) != 0, "IPv4-key mode needs the IPv4 feature");
 	constexpr int NW = QT_WAVES(W);
@@ -237,6 +333,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		sub = SWZ ? ((uint32_t)lane >> 3) & 3 : c % CPP;
 	};
 	const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+	static_assert(!CW || (W == 64 && !WIDE && !V6), "the count wave: u16 logs, 64-byte windows");
+	const bool cwv = CW && wv == NW;   // (the count wave: no classify work)
 	// the index, in scalar registers
 	const uint64_t qb = rfl64((uint64_t)(uintptr_t)a.qt);
 	const uint32_t qbits = rfl(a.qt_bits), qseed = rfl(a.qt_seed);
@@ -323,7 +421,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// (counters, port image, log rings) and its barrier
 	u32x4 preA[CPP], preB[CPP], preC[D == 3 ? CPP : 1];
 	len_t lenA = 0, lenB = 0, lenC = 0;
-	if (nt) {
+	if (nt && !cwv) {
 		issue(tileOf(0), preA, lenA);
 		__builtin_amdgcn_sched_barrier(0);
 		issue(tileOf(1), preB, lenB);
@@ -400,7 +498,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 					if (ql & !ok)
 						atomicSub(&s_res[p], 1u);
 					if ((q & !ok) && !cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
-						gatomic_add32(a.qt_hits + qs, 1u);
+						gatomic_add32(a.qt_hitx + qs, 1u);
 					if (dc & !ps)
 						atomicAdd(&cn.dcnt[tag], 1u);
 					cn.bump(a, pick(q | dc | ps, CT_NONE, tag), lane);
@@ -428,7 +526,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 				}
 				// the ring full (or no log): the LDS counter cache
 				if (!ring && !cache_hit(cn.ctag, cn.ccnt, QTAG | qs, 1))
-					gatomic_add32(a.qt_hits + qs, 1u);
+					gatomic_add32(a.qt_hitx + qs, 1u);
 			}
 		}
 		if constexpr (PORTS)
@@ -456,7 +554,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			} else {
 				const uint32_t g = ((e >> 4) << 12) | (p << 4) | (e & 15);
 				if (!cache_hit(cn.ctag, cn.ccnt, QTAG | g, 1))
-					gatomic_add32(a.qt_hits + g, 1u);
+					gatomic_add32(a.qt_hitx + g, 1u);
 			}
 		}
 	};
@@ -543,22 +641,49 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	u32x4 bs0 = { 0, 0, 0, 0 }, bs1 = { 0, 0, 0, 0 };
 	// one bucket's 16 entries (halves in lanes i and i + 32 of h0 / h1, see
 	// L) searched for entry q: found, its index, the overflow marker
-	auto match = [](const u32x4 &h0, const u32x4 &h1, uint32_t q, bool &found, uint32_t &ix) {
+	auto match = [](u32x4 &h0, u32x4 &h1, uint32_t q, bool &found, uint32_t &ix) {
 		uint32_t w[8];
 #pragma unroll
 		for (int c = 0; c < 4; c++) {
+#if XFG_QT_PLIP   /* the swap in place: the halves are dead after the match (no copies) */
+			uint32_t x = h0[c], y = h1[c];
+			asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+			w[c] = x;
+			w[4 + c] = y;
+#else
 			const auto sw = __builtin_amdgcn_permlane32_swap(h0[c], h1[c], false, false);
 			w[c] = sw[0];
 			w[4 + c] = sw[1];
+#endif
 		}
-		found = false;
-		ix = 0;
+		if constexpr (XFG_QT_PKM) {
+			// entry e's half of w[e / 2] xor q is zero where it matches;
+			// min(half, 1) per half (v_pk_min_u16) is 0 there, 1 elsewhere
+			// -- dword i's two results at bits 2i and 2i + 16 of N, the
+			// matching entry the lowest clear even bit (bit b: entry
+			// 2 (b & 14) / 2 + b / 16); keys are unique, at most one matches
+			const uint32_t qq = q * 0x10001u;
+			uint32_t nm = 0;
 #pragma unroll
-		for (int i = 0; i < 8; i++) {
-			const bool lo = (w[i] & 0xffffu) == q, hi = (w[i] >> 16) == q;
-			found |= lo | hi;
-			ix = pick(lo, 2u * i, ix);
-			ix = pick(hi, 2u * i + 1, ix);
+			for (int i = 0; i < 8; i++) {
+				uint32_t m;
+				asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(w[i] ^ qq), "s"(0x10001u));
+				nm |= m << (2 * i);
+			}
+			const uint32_t hitm = ~nm & 0x55555555u;
+			found = hitm != 0;
+			const uint32_t b = (uint32_t)__builtin_ctz(hitm | 0x80000000u);
+			ix = (b & 14u) | (b >> 4);
+		} else {
+			found = false;
+			ix = 0;
+#pragma unroll
+			for (int i = 0; i < 8; i++) {
+				const bool lo = (w[i] & 0xffffu) == q, hi = (w[i] >> 16) == q;
+				found |= lo | hi;
+				ix = pick(lo, 2u * i, ix);
+				ix = pick(hi, 2u * i + 1, ix);
+			}
 		}
 		return (w[7] >> 16) == XFG_QT_OVF_MARK;
 	};
@@ -1017,7 +1142,10 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 		else if constexpr (D == 3)
 			iteration(k, preC, lenC, rs, u % 2 == 0);
 	};
-	if constexpr (D == 2) {
+	if (cwv) {
+		if constexpr (CW)   // (past the direct counters: the histogram)
+			qt_count_wave(a, (lds_u32 *)(dcnt_base(a, s_dyn) + ((a.dcnt + 3) & ~3u)));
+	} else if constexpr (D == 2) {
 		uint32_t k = 0;
 		for (; k + 1 < iters; k += 2) {
 			iteration(k, preA, lenA, stA, true);
@@ -1064,7 +1192,7 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 	// the deferred packets: the whole reference walk over the canonical
 	// table (classify_staged), 64 at a time -- or listed for
 	// xfg_defer_kernel, which takes every wave's list after this kernel
-	if (a.defer_sep) {
+	if (a.defer_sep && !cwv) {
 		if (lane == 0)
 			a.defer_n[blockIdx.x * NW + wv] = ndef;
 		ndef = 0;
@@ -1092,13 +1220,13 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			atomicAdd(&s_stats[2 * kk + 1], x);
 		}
 	}
-	if (lane == 0)
+	if (lane == 0 && !cwv)
 		s_tn[wv] = tn;
 	__syncthreads();
 	// (every wave's appends are done: done == head) the rest of this
 	// wave's partitions, and the slices' fills for the count kernel; a
 	// position past a slice goes to the counter cache, flushed below
-	if (a.pbuf && !(dg & 16)) {
+	if (a.pbuf && !(dg & 16) && !cwv) {
 		const uint32_t hd = (uint32_t)lane < pcnt ? s_hd[2 * wc_p] : 0u;
 		// (every position within its slice -- the usual case: two rings
 		// per instruction, 8 bytes a lane, one LDS read and one store each
@@ -1139,6 +1267,8 @@ __global__ __launch_bounds__(QT_THREADS(W), QT_MINW(W)) void xfg_pipeq_kernel(co
 			gst32(a.pfill + (uint64_t)wc_p * a.pslices + a.pslice0 + blockIdx.x, hd);
 	}
 	__syncthreads();
+	if (cwv)
+		return;
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
 	cn.flush(a, tid, NT);
