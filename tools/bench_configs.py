@@ -11,6 +11,9 @@
   c3  C3 itself at SURVEY.md §8d's 2^24 batch (bench.py times 2^26)
   c3sd  C3 with every rule src|dst (`-m src,dst`): both IPv4 lookups live,
       so a packet probes two keys (the case C3's all-dst census skips)
+  c3e  C3 plus C1's 8 MAC rules (4 dst, 4 src; a ruled MAC in 10 % of the
+      frames): Ethernet rules beside IP rules, the generic pipelined kernel
+      with the Ethernet map as its LDS key table
 
   c1  xdpfilt_alw_eth, the 8 MAC rules 02:00:00:00:00:0{1..8} (4 dst, 4
       src), 64 B Ethernet/IPv4/UDP frames, 25% carrying a ruled MAC (SURVEY.md
@@ -100,8 +103,8 @@ def run(name, args):
     import xfgpu as G
     if name == "c1":
         return run_c1(args)
-    kind = {"c2": 2, "c3": 3, "c4": 4, "c5": 5, "c3sd": 3}[name]
-    n = 1 << (args.log2_packets or {"c2": 24, "c3": 24, "c4": 23, "c5": 23, "c3sd": 24}[name])
+    kind = {"c2": 2, "c3": 3, "c4": 4, "c5": 5, "c3sd": 3, "c3e": 3}[name]
+    n = 1 << (args.log2_packets or {"c2": 24, "c3": 24, "c4": 23, "c5": 23, "c3sd": 24, "c3e": 24}[name])
     stride = 64 if kind in (2, 3) else 1536
     n4 = {2: 1000, 3: 1_000_000, 4: 1_000_000, 5: 15_000_000}[kind]
     flag = 3 if name == "c3sd" else 2
@@ -122,6 +125,16 @@ def run(name, args):
     if kind != 2:
         pk = np.array([X.port_key(int(p)) for p in ports], "<u4").view(np.uint8)
         f.update_batch(G.MAP_PORTS, pk, np.full(len(ports), 2 | 4 | 8, np.uint64))
+    if name == "c3e":   # C1's MAC rules, a ruled MAC where its rule looks in 10 % of the frames
+        er = X.c1_rules().prepared()
+        f.update_batch(G.MAP_ETHERNET, er.eth_keys, er.eth_vals)
+        rng = np.random.default_rng(9)
+        d = data.reshape(n, stride)
+        pick = rng.choice(n, n // 10, replace=False)
+        which = rng.integers(0, len(er.eth_keys), len(pick))
+        dst = (er.eth_vals[which] & 2) != 0
+        d[pick[dst], 0:6] = er.eth_keys[which[dst]]
+        d[pick[~dst], 6:12] = er.eth_keys[which[~dst]]
     setup_s = time.time() - t0
     print(f"[{name}] rules loaded {setup_s:.1f}s", file=sys.stderr, flush=True)
     alg = int(np.minimum(lens.astype(np.int64), 128).sum() + n)
@@ -131,6 +144,7 @@ def run(name, args):
     f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, 2)
     ms = f.classify_timed(d_data.ptr, d_lens.ptr, n, stride, d_verd.ptr, args.iters)
     line = {"config": name, "program": f.prog_name, "packets": n, "stride": stride,
+            "kernel_path": f.last_path(),
             "rules_ipv4": n4, "rules_ipv6": n6, "port_rules": nports if kind != 2 else 0,
             "kernel_ms": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
             "roofline": {"alg_bytes_per_launch": alg,

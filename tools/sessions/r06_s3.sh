@@ -27,4 +27,17 @@ tail -2 $OUT/${T}_smoke.log
 echo "== bench"
 step 400 python bench.py > $OUT/${T}_bench.log 2>&1 || { tail -20 $OUT/${T}_bench.log; exit 5; }
 tail -1 $OUT/${T}_bench.log > $OUT/${T}_bench_c3.json; python3 -c "import json;d=json.load(open('$OUT/${T}_bench_c3.json'));print(d['ms_per_step'],d['roofline']['frac'],d['roofline']['kernel_ms'],d['roofline']['peak_measured_stream_read'],d.get('host_path',{}))"
+T=s4
+echo "== configs"
+step 900 python3 tools/bench_configs.py c2 c3 c4 c5 c3sd c1 c3e > $OUT/${T}_configs.log 2>&1 || { tail -5 $OUT/${T}_configs.log; exit 7; }
+grep '"config"' $OUT/${T}_configs.log | cut -c1-330
+echo "== per-GPU shard sizes"
+for c in c3 c4; do
+	for l in 21 22; do
+		step 300 python3 tools/bench_configs.py $c --log2-packets $l > $OUT/${T}_${c}_$l.log 2>&1 || exit 3
+		echo "$c 2^$l cw $(grep -o '"kernel_path": [0-9]*, \|"kernel_ms": [0-9.]*' $OUT/${T}_${c}_$l.log | tr '\n' ' ') $(grep -o '"frac": [0-9.]*' $OUT/${T}_${c}_$l.log)"
+		XFG_LIB=diag XFG_CW=off step 300 python3 tools/bench_configs.py $c --log2-packets $l > $OUT/${T}_${c}_${l}_off.log 2>&1 || exit 3
+		echo "$c 2^$l off $(grep -o '"kernel_ms": [0-9.]*' $OUT/${T}_${c}_${l}_off.log) $(grep -o '"frac": [0-9.]*' $OUT/${T}_${c}_${l}_off.log)"
+	done
+done
 echo ${T} done

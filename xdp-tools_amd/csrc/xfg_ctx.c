@@ -518,6 +518,9 @@ static int dev_init(xfg_ctx *ctx, struct xfg_dev *d)
 					(c & 1 ? XFG_DCNT_MAX * 4 : 0) + (c & 2 ? XFG_PORT_NIB_WORDS * 4 : 0) +
 					(c & 4 ? XFG_BLOOM_LDS_MAX * 4 : 0) + (c & 8 ? 12 + XFG_EK_SLOTS_MAX * 16 : 0) +
 					(k == 7 ? 16 + XFG_CW_HIST_MAX * 4 : 0));
+	/* (a query past the LDS a workgroup can have may leave an error behind:
+	 * not a launch's) */
+	(void)hipGetLastError();
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 fail:
@@ -1738,8 +1741,24 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		 * through its LDS counter cache and atomics instead) */
 		if (log_no)
 			a.qt = NULL;
-		else if (nolog || g5 > XFG_LOG_SLICES_MAX || !qt_log_fits(d->qt_n, d->qt_live == 3) ||
-			 2 * (uint64_t)d->qt_n > a.n)
+		/* (with the count wave the log's count costs the launch nothing:
+		 * then the log from XFG_CW_LOG_MIN packets instead of twice the
+		 * QT slots -- the atomics it saves are the slow part at C4's
+		 * per-GPU shard of 2^21 packets) */
+		const int occ_c5 = (a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0);
+		const int cw_cap = qt_log_hist(d->qt_n) <= XFG_CW_HIST_MAX && a.window <= 64 && !a.v6d &&
+				   2 * g5 <= XFG_LOG_SLICES_MAX && d->occ[7][0][occ_c5] > 0;
+		uint64_t cw_min = XFG_CW_LOG_MIN;
+#ifdef XFG_DIAG
+		const char *cm2 = getenv("XFG_CW_LOG_MIN");   /* packets from which the count wave's log runs */
+		if (cm2 && *cm2)
+			cw_min = strtoull(cm2, NULL, 0);
+		const char *cwo = getenv("XFG_CW");
+		if (cwo && !strcmp(cwo, "off"))
+			cw_min = ~0ull;
+#endif
+		if (nolog || g5 > XFG_LOG_SLICES_MAX || !qt_log_fits(d->qt_n, d->qt_live == 3) ||
+		    (2 * (uint64_t)d->qt_n > a.n && !(cw_cap && a.n >= cw_min)))
 			qt_nolog = 1;
 		/* (the log from twice as many packets as QT slots: at as many, C3's
 		 * and C4's 1M rules at 2^21 packets ran 0.068 / 0.088 ms with it and
@@ -1910,8 +1929,12 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * XFG_CW_HIST_MAX (C3's 1M rules: 8192), no IPv6 lookups in the loop,
 	 * and the kernel launchable with its histogram */
 	const int occ_c = (a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0);
+	/* (measured, profiles/r06_s2_session.log: C3 at 2^24 0.294 against
+	 * 0.299 ms a launch; at 2^26 no better -- there the count kernel's
+	 * cost is its proportional part, which the count wave pays inside the
+	 * launch: it runs below XFG_CW_MAX_PACKETS) */
 	int cw = logs && a.qt && !pwide && hist <= XFG_CW_HIST_MAX && a.window <= 64 && !a.v6p &&
-		 2 * grid <= XFG_LOG_SLICES_MAX && d->occ[7][0][occ_c] > 0;
+		 2 * grid <= XFG_LOG_SLICES_MAX && d->occ[7][0][occ_c] > 0 && a.n < XFG_CW_MAX_PACKETS;
 #ifdef XFG_DIAG
 	const char *cwe = getenv("XFG_CW");   /* "off": the count kernel every XFG_LOG_PEND launches */
 	if (cwe && !strcmp(cwe, "off"))

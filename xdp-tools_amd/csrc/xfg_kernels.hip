@@ -38,6 +38,19 @@
 
 #include "xfg_layout.h"
 
+// Split build (xdp-tools_amd/Makefile): the same file compiled as several
+// translation units in parallel, XFG_PART_MASK choosing the programs whose
+// kernels one instantiates (bit i: program i of xfg_lc_<i> below) and
+// XFG_PART_COMMON the unit with the shared kernels and the C ABI dispatch.
+// Unset (tools/abbuild.sh, one unit): every program, the shared part too.
+#ifndef XFG_PART_MASK
+#define XFG_PART_MASK 0x3ffu
+#define XFG_PART_COMMON 1
+#endif
+#ifndef XFG_PART_COMMON
+#define XFG_PART_COMMON 0
+#endif
+
 namespace {
 
 constexpr uint32_t F_TCP = 1u << 0;
@@ -1290,6 +1303,7 @@ __global__ __launch_bounds__(TILE) void xfg_classify_kernel(const xfg_kargs a)
 // stores.  A wave per slice, eight slices in flight per wave, one 8-byte
 // load per lane (a wave load covers 256 entries: about a uniform slice, so
 // few of the LDS atomics' lanes idle).
+#if XFG_PART_COMMON
 constexpr int LC_THREADS = 1024;
 #ifndef XFG_LC_U   /* slices a wave has in flight (A/B) */
 #define XFG_LC_U 8
@@ -1415,6 +1429,8 @@ __global__ __launch_bounds__(LC_THREADS) void xfg_log_count_kernel(const xfg_kar
 		}
 	}
 }
+
+#endif   // XFG_PART_COMMON
 
 #ifdef XFG_DIAG   // (1-3 % slower than each wave's tail: DESIGN.md §5.3; diagnostics only)
 // ---------------------------------------------------------------- deferred packets
@@ -1679,6 +1695,7 @@ hipError_t launch_feat(const xfg_kargs &a, unsigned grid, hipStream_t s)
 #define XFG_ALL (F_TCP | F_UDP | F_IPV6 | F_IPV4 | F_ETH)
 #define XFG_ALLOW (1u << 5)
 
+#if XFG_PART_COMMON
 // The hit log's count kernel (after a classify that filled a.pbuf / a.pfill,
 // on the same stream: overlapping it with the next classify on a second
 // stream slowed the classify)
@@ -1687,41 +1704,60 @@ extern "C" int xfg_launch_log_count(const struct xfg_kargs *a, void *stream)
 	if (!a->pbuf)
 		return 0;
 	const uint32_t passes = (a->log_span + a->log_hist - 1) / a->log_hist;
+	(void)hipGetLastError();   // (a stale error is not this launch's)
 	hipLaunchKernelGGL(xfg_log_count_kernel, dim3(XFG_LOG_PARTS * passes), dim3(LC_THREADS),
 			   (size_t)a->log_hist * 4, static_cast<hipStream_t>(stream), *a, a->log_hist);
 	const hipError_t e = hipGetLastError();
 	return e == hipSuccess ? 0 : -(int)e - 1000;
 }
+#endif
 
+// The ten programs (xfg_lc_<i> / xfg_oc_<i>: launch and occupancy of
+// program i, defined by the unit whose XFG_PART_MASK has bit i).  The A/B
+// variant libraries instantiate C3's program (XFG_AB_C3) or the Ethernet
+// programs (XFG_AB_ETH) only.
+#if defined(XFG_AB_C3)
+#define XFG_AB_OK(i) ((i) == 8)
+#elif defined(XFG_AB_ETH)
+#define XFG_AB_OK(i) ((i) == 6 || (i) == 7)
+#else
+#define XFG_AB_OK(i) 1
+#endif
+#define XFG_PROGS(X)                                     \
+	X(0, F_UDP | F_DENY)                             \
+	X(1, F_TCP | F_DENY)                             \
+	X(2, F_IPV4 | F_IPV6 | F_DENY)                   \
+	X(3, F_UDP | XFG_ALLOW)                          \
+	X(4, F_TCP | XFG_ALLOW)                          \
+	X(5, F_IPV4 | F_IPV6 | XFG_ALLOW)                \
+	X(6, F_ETH | F_DENY)                             \
+	X(7, F_ETH | XFG_ALLOW)                          \
+	X(8, XFG_ALL | F_DENY)                           \
+	X(9, XFG_ALL | XFG_ALLOW)
+#define XFG_DECL(i, F)                                                                              \
+	extern "C" hipError_t xfg_lc_##i(const xfg_kargs &a, unsigned grid, hipStream_t s);        \
+	extern "C" int xfg_oc_##i(int kind, uint32_t window, size_t dyn);
+XFG_PROGS(XFG_DECL)
+
+#if XFG_PART_COMMON
 extern "C" int xfg_launch_classify(uint32_t prog_features, const struct xfg_kargs *a,
 				   unsigned grid, void *stream)
 {
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	hipError_t e;
+	(void)hipGetLastError();   // (a stale error is not this launch's)
 	switch (prog_features) {
-#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)   /* (A/B variant libraries: C3's or the Ethernet programs only) */
-	case F_UDP | F_DENY:               e = launch_feat<F_UDP | F_DENY>(*a, grid, s); break;
-	case F_TCP | F_DENY:               e = launch_feat<F_TCP | F_DENY>(*a, grid, s); break;
-	case F_IPV4 | F_IPV6 | F_DENY:     e = launch_feat<F_IPV4 | F_IPV6 | F_DENY>(*a, grid, s); break;
-	case F_UDP | XFG_ALLOW:            e = launch_feat<F_UDP | XFG_ALLOW>(*a, grid, s); break;
-	case F_TCP | XFG_ALLOW:            e = launch_feat<F_TCP | XFG_ALLOW>(*a, grid, s); break;
-	case F_IPV4 | F_IPV6 | XFG_ALLOW:  e = launch_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(*a, grid, s); break;
-#endif
-#ifndef XFG_AB_C3
-	case F_ETH | F_DENY:               e = launch_feat<F_ETH | F_DENY>(*a, grid, s); break;
-	case F_ETH | XFG_ALLOW:            e = launch_feat<F_ETH | XFG_ALLOW>(*a, grid, s); break;
-#endif
-#ifndef XFG_AB_ETH
-	case XFG_ALL | F_DENY:             e = launch_feat<XFG_ALL | F_DENY>(*a, grid, s); break;
-#endif
-#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)
-	case XFG_ALL | XFG_ALLOW:          e = launch_feat<XFG_ALL | XFG_ALLOW>(*a, grid, s); break;
-#endif
+#define XFG_CASE_L(i, F) \
+	case F:                  \
+		e = xfg_lc_##i(*a, grid, s); \
+		break;
+	XFG_PROGS(XFG_CASE_L)
 	default:
 		return -22; /* -EINVAL */
 	}
 	return e == hipSuccess ? 0 : -(int)e - 1000;
 }
+#endif
 
 // Resident workgroups per CU of the quotient-index kernel with its count
 // wave, `dyn` bytes of dynamic LDS (the direct counters, the port map, the
@@ -1842,27 +1878,82 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 	return e == hipSuccess && n > 0 ? n : 1;
 }
 
+// Each program's entry points, in the unit that owns it (XFG_PART_MASK);
+// a program the A/B macros leave out gets stubs.
+#define XFG_DEF(i, F)                                                                               \
+	extern "C" hipError_t xfg_lc_##i(const xfg_kargs &a, unsigned grid, hipStream_t s)          \
+	{                                                                                           \
+		return launch_feat<F>(a, grid, s);                                                  \
+	}                                                                                           \
+	extern "C" int xfg_oc_##i(int kind, uint32_t window, size_t dyn)                            \
+	{                                                                                           \
+		return occupancy_feat<F>(kind, window, dyn);                                        \
+	}
+#define XFG_STUB(i)                                                                                 \
+	extern "C" hipError_t xfg_lc_##i(const xfg_kargs &, unsigned, hipStream_t)                  \
+	{                                                                                           \
+		return hipErrorInvalidValue;                                                        \
+	}                                                                                           \
+	extern "C" int xfg_oc_##i(int, uint32_t, size_t) { return 1; }
+#if ((XFG_PART_MASK >> 0) & 1) && XFG_AB_OK(0)
+XFG_DEF(0, F_UDP | F_DENY)
+#elif ((XFG_PART_MASK >> 0) & 1)
+XFG_STUB(0)
+#endif
+#if ((XFG_PART_MASK >> 1) & 1) && XFG_AB_OK(1)
+XFG_DEF(1, F_TCP | F_DENY)
+#elif ((XFG_PART_MASK >> 1) & 1)
+XFG_STUB(1)
+#endif
+#if ((XFG_PART_MASK >> 2) & 1) && XFG_AB_OK(2)
+XFG_DEF(2, F_IPV4 | F_IPV6 | F_DENY)
+#elif ((XFG_PART_MASK >> 2) & 1)
+XFG_STUB(2)
+#endif
+#if ((XFG_PART_MASK >> 3) & 1) && XFG_AB_OK(3)
+XFG_DEF(3, F_UDP | XFG_ALLOW)
+#elif ((XFG_PART_MASK >> 3) & 1)
+XFG_STUB(3)
+#endif
+#if ((XFG_PART_MASK >> 4) & 1) && XFG_AB_OK(4)
+XFG_DEF(4, F_TCP | XFG_ALLOW)
+#elif ((XFG_PART_MASK >> 4) & 1)
+XFG_STUB(4)
+#endif
+#if ((XFG_PART_MASK >> 5) & 1) && XFG_AB_OK(5)
+XFG_DEF(5, F_IPV4 | F_IPV6 | XFG_ALLOW)
+#elif ((XFG_PART_MASK >> 5) & 1)
+XFG_STUB(5)
+#endif
+#if ((XFG_PART_MASK >> 6) & 1) && XFG_AB_OK(6)
+XFG_DEF(6, F_ETH | F_DENY)
+#elif ((XFG_PART_MASK >> 6) & 1)
+XFG_STUB(6)
+#endif
+#if ((XFG_PART_MASK >> 7) & 1) && XFG_AB_OK(7)
+XFG_DEF(7, F_ETH | XFG_ALLOW)
+#elif ((XFG_PART_MASK >> 7) & 1)
+XFG_STUB(7)
+#endif
+#if ((XFG_PART_MASK >> 8) & 1) && XFG_AB_OK(8)
+XFG_DEF(8, XFG_ALL | F_DENY)
+#elif ((XFG_PART_MASK >> 8) & 1)
+XFG_STUB(8)
+#endif
+#if ((XFG_PART_MASK >> 9) & 1) && XFG_AB_OK(9)
+XFG_DEF(9, XFG_ALL | XFG_ALLOW)
+#elif ((XFG_PART_MASK >> 9) & 1)
+XFG_STUB(9)
+#endif
+
+#if XFG_PART_COMMON
 extern "C" int xfg_classify_occupancy(uint32_t prog_features, int kind, uint32_t window, size_t dyn)
 {
 	switch (prog_features) {
-#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)   /* (A/B variant libraries: C3's or the Ethernet programs only) */
-	case F_UDP | F_DENY:               return occupancy_feat<F_UDP | F_DENY>(kind, window, dyn);
-	case F_TCP | F_DENY:               return occupancy_feat<F_TCP | F_DENY>(kind, window, dyn);
-	case F_IPV4 | F_IPV6 | F_DENY:     return occupancy_feat<F_IPV4 | F_IPV6 | F_DENY>(kind, window, dyn);
-	case F_UDP | XFG_ALLOW:            return occupancy_feat<F_UDP | XFG_ALLOW>(kind, window, dyn);
-	case F_TCP | XFG_ALLOW:            return occupancy_feat<F_TCP | XFG_ALLOW>(kind, window, dyn);
-	case F_IPV4 | F_IPV6 | XFG_ALLOW:  return occupancy_feat<F_IPV4 | F_IPV6 | XFG_ALLOW>(kind, window, dyn);
-#endif
-#ifndef XFG_AB_C3
-	case F_ETH | F_DENY:               return occupancy_feat<F_ETH | F_DENY>(kind, window, dyn);
-	case F_ETH | XFG_ALLOW:            return occupancy_feat<F_ETH | XFG_ALLOW>(kind, window, dyn);
-#endif
-#ifndef XFG_AB_ETH
-	case XFG_ALL | F_DENY:             return occupancy_feat<XFG_ALL | F_DENY>(kind, window, dyn);
-#endif
-#if !defined(XFG_AB_C3) && !defined(XFG_AB_ETH)
-	case XFG_ALL | XFG_ALLOW:          return occupancy_feat<XFG_ALL | XFG_ALLOW>(kind, window, dyn);
-#endif
+#define XFG_CASE_O(i, F) \
+	case F:                  \
+		return xfg_oc_##i(kind, window, dyn);
+	XFG_PROGS(XFG_CASE_O)
 	default:                          return 1;
 	}
 }
@@ -1895,6 +1986,7 @@ __global__ __launch_bounds__(256) void xfg_stream_read_kernel(const u32x4 *__res
 extern "C" int xfg_launch_stream_read(const void *src, uint64_t bytes, void *sink,
 				      unsigned grid, void *stream)
 {
+	(void)hipGetLastError();
 	hipLaunchKernelGGL(xfg_stream_read_kernel, dim3(grid), dim3(256), 0,
 			   static_cast<hipStream_t>(stream), static_cast<const u32x4 *>(src),
 			   bytes / 16, static_cast<u32x4 *>(sink));
@@ -1923,6 +2015,7 @@ extern "C" int xfg_launch_qt_fold(uint32_t *qt_hits, const uint32_t *trans,
 				  unsigned long long *hits, uint32_t n, void *stream)
 {
 	const uint32_t grid = n ? (n + 255) / 256 < 2048u ? (n + 255) / 256 : 2048u : 1u;
+	(void)hipGetLastError();
 	hipLaunchKernelGGL(xfg_qt_fold_kernel, dim3(grid), dim3(256), 0,
 			   static_cast<hipStream_t>(stream), qt_hits, trans, hits, n);
 	return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -2065,6 +2158,7 @@ extern "C" int xfg_launch_compact(const uint8_t *verdicts, uint64_t n, uint32_t 
 		return -5;
 	if (!n)
 		return hipMemsetAsync(count, 0, 8, s) == hipSuccess ? 0 : -5;
+	(void)hipGetLastError();
 	hipLaunchKernelGGL(xfg_compact_kernel, dim3(grid), dim3(CT_LANES), 0, s, verdicts, n, action,
 			   idx, count, status, ticket, ntiles);
 	return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -2074,3 +2168,5 @@ extern "C" uint64_t xfg_compact_tiles(uint64_t n)
 {
 	return (n + CT_TILE - 1) / CT_TILE;
 }
+
+#endif   // XFG_PART_COMMON

@@ -102,6 +102,8 @@
 #define XFG_LOG_PARTS     256u    /* hit-log partitions (16-counter chunks dealt round-robin) */
 #define XFG_LOG_HIST_MAX  16384u  /* count-kernel LDS histogram entries (64 KiB) */
 #define XFG_CW_HIST_MAX   8192u   /* the QT kernel's count-wave histogram entries (32 KiB) */
+#define XFG_CW_LOG_MIN    (1ull << 20)   /* packets from which the count wave's log runs */
+#define XFG_CW_MAX_PACKETS (1ull << 25)   /* ... and below which it does */
 #define XFG_LOG_PASSES_MAX 32u    /* histogram passes per partition (span 512K) */
 #define XFG_LOG_SLICES_MAX 1024u  /* slices per partition: classify workgroups */
 #define XFG_DEFER_SRC_MAX 4096u   /* deferred lists (classify waves) xfg_defer_kernel takes */

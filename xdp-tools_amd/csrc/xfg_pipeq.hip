@@ -88,8 +88,9 @@
 #ifndef XFG_QT_CNT2      /* 1: the hit's ring atomics without exec masks (a word per lane past the rings) */
 #define XFG_QT_CNT2 1
 #endif
-#ifndef XFG_QT_PKM       /* 1: the bucket match by packed u16 min (no compare masks in SGPRs) */
-#define XFG_QT_PKM 1
+#ifndef XFG_QT_PKM       /* 1: the bucket match by packed u16 min (no compare masks in SGPRs; A/B:
+			    16 fewer SALU and 4 more VALU a tile, 0.5-0.7 % slower at 2^26, r06_s2) */
+#define XFG_QT_PKM 0
 #endif
 #ifndef XFG_QT_PLIP      /* 1: the bucket halves swapped in place by inline asm */
 #define XFG_QT_PLIP 0
