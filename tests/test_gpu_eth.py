@@ -228,8 +228,10 @@ def test_eth_table_beside_ip_rules(G, variant, stride):
     verdicts, every rule value and the stats equal the restatement's."""
     rules, pool = X.random_rules(311 + stride, n4=20000, n6=2000, ne=12, nports=30)
     n = 200000 if stride == 64 else 30000
-    data, lens = X.gen_fuzz(312 + stride, n, stride, rules, pool)
-    d = data.reshape(n, stride)
+    gs = max(stride, 160)   # (the fuzz generator's slot; a 64-byte slot takes each frame's head)
+    g, gl = X.gen_fuzz(312 + stride, n, gs, rules, pool)
+    d = np.ascontiguousarray(g.reshape(n, gs)[:, :stride])
+    data, lens = d.reshape(-1), np.minimum(gl, stride).astype(np.uint32)
     rng = np.random.default_rng(313)
     k = rules.eth_keys
     dst = rng.choice(n, n // 8, replace=False)

@@ -550,7 +550,7 @@ def test_classify_host_registered_unaligned(G, shift):
     """A registered buffer whose batch does not start 16-byte aligned: the
     zero-copy path (16-byte loads in place) needs aligned slots, so the
     batch takes the staged path -- results equal to the restatement."""
-    n, stride = 200000, 64
+    n, stride = 200000, 160
     rules, pool = X.random_rules(91 + shift, n4=300, n6=100, ne=20, nports=40)
     data, lens = X.gen_fuzz(17 + shift, n, stride, rules, pool)
     buf = np.zeros(n * stride + 64, np.uint8)
@@ -564,12 +564,27 @@ def test_classify_host_registered_unaligned(G, shift):
     f.load_rules(rules)
     f.host_register(buf)
     try:
-        v = f.classify_host(sub, lens.astype(np.uint16), stride=stride)
+        v = f.classify_host(sub, lens, stride=stride)
     finally:
         f.host_unregister(buf)
     np.testing.assert_array_equal(v, ov)
     np.testing.assert_array_equal(f.stats(), ost)
     f.close()
+
+
+@pytest.mark.timeout(300)
+def test_classify_host_registered_hybrid():
+    """Registered 1536-byte slots through the hybrid host path -- each round
+    a zero-copy chunk and staged chunks of header windows, side by side
+    (xfg_ctx.c host_run_hyb) -- equal to the restatement; run in a fresh
+    process on the diagnostics library with the rounds made small enough
+    (XFG_HYB_ZLOG2=16) for a test-sized batch (tests/gpu_hyb_worker.py)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, XFG_LIB="diag", XFG_HYB_ZLOG2="16", XFG_HYB_ST="2")
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gpu_hyb_worker.py")],
+                       capture_output=True, text=True, timeout=280, env=env)
+    assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
 
 
 def test_classify_host_registered_large_slots_many_frames(G):

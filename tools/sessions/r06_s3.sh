@@ -14,10 +14,6 @@ step() {
 	return $rc
 }
 cd $R
-echo "== count-wave parity over several launches (product library)"
-for args in "--reps 5" "--reps 5 --src-dst" "--reps 4 --hot 8" "--reps 3 --log2-packets 24"; do
-	XFG_LIB=$R/xdp-tools_amd/lib/libxdpfilter_gpu.so step 300 python3 tools/ab_parity.py $args || exit 2
-done
 echo "== GPU suite"
 step 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $OUT/${T}_pytest_gpu.log 2>&1
 rc=$?; tail -3 $OUT/${T}_pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" $OUT/${T}_pytest_gpu.log | head -30; exit $rc; }

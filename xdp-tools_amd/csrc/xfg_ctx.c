@@ -2541,6 +2541,12 @@ static int host_registered(xfg_ctx *ctx, const void *p, uint64_t bytes, const ui
  * of its time (C3, u32 lengths: 2^18-packet chunks 430 Mpps, 2^21 630, one
  * launch from device-resident lengths 790). */
 #define ZC_CH (1u << 21)   /* AF_XDP (13 bytes a packet); fixed stride: twice (5 bytes) */
+#ifndef HYB_ZC_CH   /* host_run_hyb: packets of a round's zero-copy chunk, ... */
+#define HYB_ZC_CH (1ull << 20)
+#endif
+#ifndef HYB_ST_N    /* ... and its staged chunks of HOST_CH (0: no hybrid) */
+#define HYB_ST_N 2u
+#endif
 _Static_assert((size_t)ZC_CH * 13 + 256 <= (size_t)HOST_CH * HOST_WIN, "slot buffers hold a chunk");
 _Static_assert((size_t)ZC_CH * 2 * 5 + 256 <= (size_t)HOST_CH * HOST_WIN, "slot buffers hold a chunk");
 
@@ -2582,6 +2588,81 @@ static int host_run_zc(xfg_ctx *ctx, struct xfg_dev *d, const struct hsrc *src, 
 	}
 	for (int k = 0; k < HOST_SLOTS; k++)
 		HIPCHK(hipStreamSynchronize(d->hs_st[k]));
+fail:
+	return err;
+}
+
+/* Registered large slots (C5's 1514-byte frames at a 1536-byte stride): the
+ * zero-copy kernels are bound by the rate of PCIe read requests (one 64-byte
+ * window a frame, ~0.3 Gpps) and the staged path by the pool's gather (~0.13
+ * Gpps), different resources -- so each round takes one zero-copy chunk of
+ * zc_ch packets (its kernel reading mapped host memory while the pool works)
+ * and then st_n staged chunks of header windows (gathered meanwhile, their
+ * kernels queued behind it): slots 0-1 for the zero-copy chunks, 2-3 for the
+ * staged ones.  Verdicts, counters and stats are those of either path: the
+ * same kernels over the same frames, the staged windows' leavers walked
+ * whole (host_fallback). */
+static int host_run_hyb(xfg_ctx *ctx, struct xfg_dev *d, const struct hsrc *src, uint64_t n,
+			const uint8_t *rbase, uint8_t *verdicts, uint64_t zc_ch, uint32_t st_n)
+{
+	int err = 0;
+	void *dp = NULL;
+	HIPCHK(hipHostGetDevicePointer(&dp, (void *)rbase, 0));
+	const uint8_t *zdev = (const uint8_t *)dp + (src->data - rbase);
+	const size_t ls = src->lens_u16 ? 2 : 4;
+	uint64_t pend[HOST_SLOTS];
+	for (int k = 0; k < HOST_SLOTS; k++)
+		pend[k] = UINT64_MAX;
+	uint32_t zk = 0, sk = 0;
+	for (uint64_t c = 0; c < n;) {
+		/* the zero-copy chunk: the pool copies its lengths, the kernel
+		 * reads the frames where they lie */
+		{
+			const int k = (int)(zk++ & 1);
+			const uint64_t m = n - c < zc_ch ? n - c : zc_ch;
+			const size_t lb = m * ls, vb = (lb + 255) & ~(size_t)255;
+			HIPCHK(hipEventSynchronize(d->hs_done[k]));
+			struct gather_job job = { src, c, m, d->hs_hbuf[k], (uint32_t *)d->hs_hbuf[k], HOST_WIN, 4 };
+			hpool_run(d->pool, gather_slice, &job);
+			HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], d->hs_hbuf[k], lb, hipMemcpyHostToDevice, d->hs_st[k]));
+			struct xfg_batch sub = { zdev + c * src->stride, NULL, d->hs_dbuf[k], m, src->stride, ls == 2 };
+			if ((err = host_launch(ctx, d, &sub, d->hs_dbuf[k] + vb, 0, NULL, NULL, d->hs_st[k])))
+				goto fail;
+			HIPCHK(hipMemcpyAsync(verdicts + c, d->hs_dbuf[k] + vb, m, hipMemcpyDeviceToHost,
+					      d->hs_st[k]));
+			HIPCHK(hipEventRecord(d->hs_done[k], d->hs_st[k]));
+			c += m;
+		}
+		/* the staged chunks: 128-byte header windows gathered by the pool
+		 * while the zero-copy kernel runs */
+		for (uint32_t j = 0; j < st_n && c < n; j++) {
+			const int k = 2 + (int)(sk++ & 1);
+			const uint64_t m = n - c < HOST_CH ? n - c : HOST_CH;
+			HIPCHK(hipEventSynchronize(d->hs_done[k]));
+			if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
+				goto fail;
+			struct gather_job job = { src, c, m, d->hs_hbuf[k], d->hs_hl[k], HOST_WIN, 0 };
+			hpool_run(d->pool, gather_slice, &job);
+			HIPCHK(hipMemcpyAsync(d->hs_dbuf[k], d->hs_hbuf[k], m * HOST_WIN, hipMemcpyHostToDevice,
+					      d->hs_st[k]));
+			HIPCHK(hipMemcpyAsync(d->hs_dl[k], d->hs_hl[k], m * 4, hipMemcpyHostToDevice, d->hs_st[k]));
+			HIPCHK(hipMemsetAsync(d->hs_fbc[k], 0, 4, d->hs_st[k]));
+			struct xfg_batch sub = { d->hs_dbuf[k], NULL, d->hs_dl[k], m, HOST_WIN, 0 };
+			if ((err = host_launch(ctx, d, &sub, d->hs_dv[k], 1, d->hs_fb[k], d->hs_fbc[k],
+					       d->hs_st[k])))
+				goto fail;
+			HIPCHK(hipMemcpyAsync(verdicts + c, d->hs_dv[k], m, hipMemcpyDeviceToHost, d->hs_st[k]));
+			HIPCHK(hipMemcpyAsync(d->hs_hfbc[k], d->hs_fbc[k], 4, hipMemcpyDeviceToHost, d->hs_st[k]));
+			HIPCHK(hipEventRecord(d->hs_done[k], d->hs_st[k]));
+			pend[k] = c;
+			c += m;
+		}
+	}
+	for (int k = 0; k < HOST_SLOTS; k++) {
+		HIPCHK(hipStreamSynchronize(d->hs_st[k]));
+		if (pend[k] != UINT64_MAX && (err = host_fallback(ctx, d, src, pend[k], k, verdicts)))
+			goto fail;
+	}
 fail:
 	return err;
 }
@@ -2634,6 +2715,23 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 	HIPCHK(hipSetDevice(d->ordinal));
 	if ((err = host_staging(d)))
 		goto fail;
+	/* (registered large slots, a batch of several rounds: zero copy and the
+	 * staged gather side by side, host_run_hyb) */
+	uint64_t hyb_zc = HYB_ZC_CH;
+	uint32_t hyb_st = HYB_ST_N;
+#ifdef XFG_DIAG
+	const char *hz = getenv("XFG_HYB_ZLOG2");   /* zero-copy chunk (log2); 0: no hybrid */
+	if (hz && *hz)
+		hyb_zc = atoi(hz) ? 1ull << atoi(hz) : 0;
+	const char *hn = getenv("XFG_HYB_ST");      /* staged chunks a round */
+	if (hn && *hn)
+		hyb_st = (uint32_t)atoi(hn);
+#endif
+	if (zc && hyb_zc && hyb_st && !src->descs && src->stride > HOST_WIN && n >= 2 * hyb_zc &&
+	    hyb_zc <= 2 * ZC_CH) {
+		err = host_run_hyb(ctx, d, src, n, rbase, verdicts, hyb_zc, hyb_st);
+		goto fail;
+	}
 	if (zc) {
 		err = host_run_zc(ctx, d, src, n, rbase, verdicts);
 		goto fail;
