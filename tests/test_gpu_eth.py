@@ -154,24 +154,17 @@ M32 = 0xffffffff
 ETH_SEED = 0x5eed1234 ^ 0xbb67ae85     # xfg_open's default seed ^ the Ethernet map's
 
 
-def _fmix32(h):
-    h = h.astype(np.uint64)
-    h ^= h >> 16
-    h = (h * 0x85ebca6b) & M32
-    h ^= h >> 13
-    h = (h * 0xc2b2ae35) & M32
-    h ^= h >> 16
-    return h
-
-
 def eth_home(keys, slots):
-    """The LDS key table's home entry of each MAC (xfg_hash_eth & (slots - 1))."""
-    k = np.ascontiguousarray(keys, np.uint8).reshape(-1, 6)
-    lo = k[:, :4].copy().view("<u4").reshape(-1).astype(np.uint64)
-    hi = (k[:, 4].astype(np.uint64) | (k[:, 5].astype(np.uint64) << 8))
-    h = _fmix32(lo ^ np.uint64(ETH_SEED))
-    h = _fmix32(h ^ hi)
-    return (h & np.uint64(slots - 1)).astype(np.int64)
+    """The LDS key table's home entry of each MAC (xfg_ek_home, xfg_layout.h:
+    multiply-shift over the MAC's two 24-bit halves, the top bits)."""
+    k = np.ascontiguousarray(keys, np.uint8).reshape(-1, 6).astype(np.uint64)
+    lo = k[:, 0] | (k[:, 1] << 8) | (k[:, 2] << 16) | (k[:, 3] << 24)
+    hi = k[:, 4] | (k[:, 5] << 8)
+    a = (lo ^ np.uint64(ETH_SEED)) & np.uint64(0xffffff)
+    b = ((lo >> np.uint64(24)) | (hi << np.uint64(8))) ^ np.uint64(ETH_SEED >> 8)
+    h = (a * np.uint64(0x9e3779) + (b & np.uint64(0xffffff)) * np.uint64(0x7f4a7b)) & np.uint64(M32)
+    lg = int(slots).bit_length() - 1
+    return (h >> np.uint64(32 - lg)).astype(np.int64)
 
 
 def test_eth_table_long_probe_chains_and_the_513th_key(G):

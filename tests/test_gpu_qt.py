@@ -602,15 +602,35 @@ def test_qt_both_ipv4_directions_ipv6_in_loop(dirs6):
     assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
 
 
-def test_qt_not_taken_with_ethernet_rules_live(G):
-    """An Ethernet rule is tested on every frame before its IP keys
-    (xdpfilt_prog.h:187-196): the index kernel, which carries IPv4 keys only,
-    does not take such a batch (the general pipelined kernel does)."""
+@pytest.mark.parametrize("variant", ["xdpfilt_dny_all", "xdpfilt_alw_all"])
+@pytest.mark.parametrize("neth,path", [(1, 5), (12, 5), (511, 5), (600, 1)])
+def test_qt_with_ethernet_rules_live(G, variant, neth, path):
+    """Ethernet rules are tested on every frame before its IP keys
+    (lookup_verdict_ethernet, xdpfilt_prog.h:187-196,224-227; a hit ends
+    the program, even for a frame whose IP header would abort).  With the
+    Ethernet map small enough for its LDS key table (at most 512 keys) the
+    index kernel takes the batch and answers both Ethernet lookups from the
+    table ahead of its IPv4 lookups (path 5); a larger map keeps the generic
+    pipelined kernel (path 1).  A fifth of the frames carry a ruled MAC in
+    the direction its rule tests, some in the other direction."""
+    rng = np.random.default_rng(111 + neth)
     rules, v4, ports = one_direction_rules(111, 20000, 2)
-    rules.eth_keys = np.array([[2, 0, 0, 0, 0, 1]], np.uint8)
-    rules.eth_vals = np.array([2], np.uint64)
-    data, lens = X.gen_workload(112, 3, 1 << 15, 64, v4=v4, ports=ports)
-    run_both(G, "xdpfilt_dny_all", rules, data, lens, 64, path=1, eth_capacity=16)
+    ek = X.rand_keys(113 + neth, neth, 6)
+    rules.eth_keys = ek
+    rules.eth_vals = rng.choice(np.array([1, 2, 3], np.uint64), len(ek)) | \
+        (rng.integers(0, 30, len(ek)).astype(np.uint64) << 6)
+    d1, l1 = X.gen_workload(112, 3, 1 << 15, 64, v4=v4, ports=ports)
+    d2, l2 = fuzz_at(114, 1 << 14, 64, rules, ports)
+    data, lens = np.concatenate([d1, d2]), np.concatenate([l1, l2])
+    d = data.reshape(-1, 64)
+    n = len(d)
+    pick = rng.choice(n, n // 5, replace=False)
+    which = rng.integers(0, len(ek), len(pick))
+    half = len(pick) // 2
+    d[pick[:half], 0:6] = ek[which[:half]]
+    d[pick[half:], 6:12] = ek[which[half:]]
+    ov = run_both(G, variant, rules, data, lens, 64, path=path, eth_capacity=1024)
+    assert len(np.unique(ov)) == 3
 
 
 @pytest.mark.timeout(300)

@@ -26,13 +26,16 @@ def main():
     v4 = X.rand_keys(5, int(n4 * 1.02) + 16, 4)[:n4]
     v6 = X.rand_keys(105, int(n6 * 1.02) + 16, 16)[:n6]
     ports = (np.arange(nports, dtype=np.uint32) * 61 + 53).astype(np.uint16)
+    t0 = time.perf_counter()
     data, lens = X.gen_workload(5, 5, n, stride, v4=v4, v6=v6, ports=ports)
+    print(f"workload {time.perf_counter() - t0:.1f} s", flush=True)
     f = G.Filter(G.FEAT_ALL | G.FEAT_DENY, devices=[0], ipv4_capacity=n4, ipv6_capacity=n6)
     f.update_batch(G.MAP_IPV4, v4, np.full(len(v4), 2, np.uint64))
     f.update_batch(G.MAP_IPV6, v6, np.full(len(v6), 2, np.uint64))
     pk = np.array([X.port_key(int(p)) for p in ports], "<u4").view(np.uint8)
     f.update_batch(G.MAP_PORTS, pk, np.full(len(ports), 2 | 4 | 8, np.uint64))
     f.host_register(data)
+    print(f"rules and registration {time.perf_counter() - t0:.1f} s", flush=True)
     ref = None
     for rnd in range(2):
         for zs in sys.argv[1:]:

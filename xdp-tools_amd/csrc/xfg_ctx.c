@@ -1471,7 +1471,7 @@ static int qt_refresh(xfg_ctx *ctx, struct xfg_dev *d, uint32_t live)
 
 /* The Ethernet map as the Ethernet-key kernel's key table (ctx->lock held):
  * rebuilt on the host after an edit, then uploaded to @d when its copy is
- * older.  A key at home xfg_hash_eth & (slots - 1), linear probing; slots
+ * older.  A key at home xfg_ek_home, linear probing; slots
  * at least twice the keys.  ek_ok 0 (the generic kernel instead): more than
  * XFG_EK_MAX_KEYS keys, or a flag byte that differs between devices. */
 static int ek_refresh(xfg_ctx *ctx, struct xfg_dev *d)
@@ -1497,7 +1497,7 @@ static int ek_refresh(xfg_ctx *ctx, struct xfg_dev *d)
 				continue;
 			uint32_t lo, hi = k[4] | (uint32_t)k[5] << 8;
 			memcpy(&lo, k, 4);
-			uint32_t e = xfg_hash_eth(lo | ((uint64_t)hi << 32), t->seed) & (sl - 1), dsp = 0;
+			uint32_t e = xfg_ek_home(lo, hi, t->seed, (uint32_t)__builtin_ctz(sl)), dsp = 0;
 			while (ctx->ek_host[4 * e + 3] & XFG_EK_VALID) {
 				e = (e + 1) & (sl - 1);
 				dsp++;
@@ -1611,11 +1611,35 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 		a->port_count = 0;
 	}
 #endif
+	/* the Ethernet-key kernel (kind 6): the Ethernet-only programs, their
+	 * map as an LDS key table -- every lookup answered in LDS, no frame
+	 * byte past the two addresses read */
+	/* (and, since round 6, for the generic pipelined kernel -- live
+	 * Ethernet keys beside IP keys: dny_all / alw_all with a few MAC rules --
+	 * which answers both Ethernet lookups from the same table in LDS) */
+	const int ek_only = !(ctx->prog_features & (XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_TCP | XFG_FEAT_UDP));
+	int ek = a->pipe && (ctx->prog_features & XFG_FEAT_ETHERNET) && (ek_only || eth_live);
+#ifdef XFG_DIAG
+	const char *eo = getenv("XFG_EK");   /* "off": the generic pipelined kernel */
+	if (eo && !strcmp(eo, "off"))
+		ek = 0;
+#endif
+	if (ek) {
+		if ((err = ek_refresh(ctx, d)))
+			return err;
+		if (ctx->ek_ok)
+			a->ek = d->ek_img;   /* (parameters: launch_batch, under d->lock) */
+	}
+	/* (live Ethernet keys, no IPv6 key, the Ethernet map as the LDS key
+	 * table: the quotient-index kernel answers the Ethernet lookups from
+	 * the table ahead of its IPv4 lookups -- since round 6; else the
+	 * generic pipelined kernel takes the batch) */
+	const int kme = (ctx->prog_features & XFG_FEAT_IPV4) && eth_live && !v6_live && a->ek && !ek_only;
 	/* the quotient index (kind 5 kernel): the IPv4-key kernel with one or
 	 * both IPv4 lookup directions live, the same flags on every device, and
 	 * a map large enough that the prefilter + bucket-line chain leaves L2;
 	 * its hit log must fit the count kernel's histogram */
-	if (a->pipe && (a->km || km6) && !a->split) {
+	if (a->pipe && (a->km || km6 || kme) && !a->split) {
 		/* (both directions live: up to two images, twice the QT slots) */
 		const int dl = a->t4.count && (a->t4.fmask & 2), sl = a->t4.count && (a->t4.fmask & 1);
 		const int ok = (dl | sl) && !ctx->flag_cnt[0][7] &&
@@ -1636,28 +1660,9 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 			a->qt = d->qt_img;   /* (parameters: launch_batch, under d->lock) */
 			if (!a->km) {
 				a->km = 1;
-				a->v6d = 1;
+				a->v6d = !kme;
 			}
 		}
-	}
-	/* the Ethernet-key kernel (kind 6): the Ethernet-only programs, their
-	 * map as an LDS key table -- every lookup answered in LDS, no frame
-	 * byte past the two addresses read */
-	/* (and, since round 6, for the generic pipelined kernel -- live
-	 * Ethernet keys beside IP keys: dny_all / alw_all with a few MAC rules --
-	 * which answers both Ethernet lookups from the same table in LDS) */
-	const int ek_only = !(ctx->prog_features & (XFG_FEAT_IPV4 | XFG_FEAT_IPV6 | XFG_FEAT_TCP | XFG_FEAT_UDP));
-	int ek = a->pipe && (ctx->prog_features & XFG_FEAT_ETHERNET) && (ek_only || eth_live);
-#ifdef XFG_DIAG
-	const char *eo = getenv("XFG_EK");   /* "off": the generic pipelined kernel */
-	if (eo && !strcmp(eo, "off"))
-		ek = 0;
-#endif
-	if (ek) {
-		if ((err = ek_refresh(ctx, d)))
-			return err;
-		if (ctx->ek_ok)
-			a->ek = d->ek_img;   /* (parameters: launch_batch, under d->lock) */
 	}
 	return 0;
 }
@@ -1732,7 +1737,8 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	int qt_nolog = 0;
 	if (a.qt) {
 		const int k5 = 5, wi5 = a.window > 64;
-		const int pc = d->occ[k5][wi5][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) | (a.bl_lds ? 4 : 0)];
+		const int pc = d->occ[k5][wi5][(a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0) | (a.bl_lds ? 4 : 0) |
+					      (a.ek ? 8 : 0)];
 		const uint64_t pw = (uint64_t)xfg_classify_threads(k5, a.window);
 		uint64_t g5 = (uint64_t)d->ncu * (pc > 0 ? pc : 1), need5 = (a.n + pw - 1) / pw;
 		if (g5 > need5)
@@ -1746,7 +1752,7 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		 * QT slots -- the atomics it saves are the slow part at C4's
 		 * per-GPU shard of 2^21 packets) */
 		const int occ_c5 = (a.dcnt > 0) | (!a.port_tab && a.port_count ? 2 : 0);
-		const int cw_cap = qt_log_hist(d->qt_n) <= XFG_CW_HIST_MAX && a.window <= 64 && !a.v6d &&
+		const int cw_cap = qt_log_hist(d->qt_n) <= XFG_CW_HIST_MAX && a.window <= 64 && !a.v6d && !a.ek &&
 				   2 * g5 <= XFG_LOG_SLICES_MAX && d->occ[7][0][occ_c5] > 0;
 		uint64_t cw_min = XFG_CW_LOG_MIN;
 #ifdef XFG_DIAG
@@ -1933,7 +1939,8 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 	 * 0.299 ms a launch; at 2^26 no better -- there the count kernel's
 	 * cost is its proportional part, which the count wave pays inside the
 	 * launch: it runs below XFG_CW_MAX_PACKETS) */
-	int cw = logs && a.qt && !pwide && hist <= XFG_CW_HIST_MAX && a.window <= 64 && !a.v6p &&
+	/* (the LDS Ethernet table and the histogram do not fit beside each other) */
+	int cw = logs && a.qt && !pwide && hist <= XFG_CW_HIST_MAX && a.window <= 64 && !a.v6p && !a.ek &&
 		 2 * grid <= XFG_LOG_SLICES_MAX && d->occ[7][0][occ_c] > 0 && a.n < XFG_CW_MAX_PACKETS;
 #ifdef XFG_DIAG
 	const char *cwe = getenv("XFG_CW");   /* "off": the count kernel every XFG_LOG_PEND launches */

@@ -1582,35 +1582,50 @@ void launch_pipeq_cw(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s
 template <uint32_t FEAT, bool L16>
 void launch_pipeq(const xfg_kargs &a, unsigned grid, size_t dl, hipStream_t s)
 {
-	if (a.cw_n) {
-		if (a.qt_live == 3)
-			launch_pipeq_cw<FEAT, L16, true>(a, grid, dl, s);
+	if constexpr ((FEAT & F_ETH) != 0) {
+		// The Ethernet lookups are compiled in only where the Ethernet map
+		// is live as the LDS key table (a.ek); otherwise every lookup would
+		// miss, and the instantiation without them runs.  The host takes the
+		// table beside IPv4 keys only: no count wave, no IPv6 in the loop.
+		if (!a.ek)
+			launch_pipeq<FEAT & ~F_ETH, L16>(a, grid, dl, s);
+		else if (a.qt_live == 3)
+			launch_pipeq2<FEAT, L16, true, false>(a, grid, dl, s);
+		else if (a.pwide)
+			launch_pipeq2<FEAT, L16, false, true>(a, grid, dl, s);
 		else
-			launch_pipeq_cw<FEAT, L16, false>(a, grid, dl, s);
-		return;
-	}
-	if constexpr ((FEAT & F_IPV6) != 0)
-		if (a.v6p) {
-			if (a.qt_live == 3 && a.v6p == 2)
-				launch_pipeq2<FEAT, L16, true, false, 2>(a, grid, dl, s);
-			else if (a.qt_live == 3)
-				launch_pipeq2<FEAT, L16, true, false, 1>(a, grid, dl, s);
-			else if (a.v6p == 2 && a.pwide)
-				launch_pipeq2<FEAT, L16, false, true, 2>(a, grid, dl, s);
-			else if (a.v6p == 2)
-				launch_pipeq2<FEAT, L16, false, false, 2>(a, grid, dl, s);
-			else if (a.pwide)
-				launch_pipeq2<FEAT, L16, false, true, 1>(a, grid, dl, s);
+			launch_pipeq2<FEAT, L16, false, false>(a, grid, dl, s);
+	} else {
+		if (a.cw_n) {
+			if (a.qt_live == 3)
+				launch_pipeq_cw<FEAT, L16, true>(a, grid, dl, s);
 			else
-				launch_pipeq2<FEAT, L16, false, false, 1>(a, grid, dl, s);
+				launch_pipeq_cw<FEAT, L16, false>(a, grid, dl, s);
 			return;
 		}
-	if (a.qt_live == 3)
-		launch_pipeq2<FEAT, L16, true, false>(a, grid, dl, s);
-	else if (a.pwide)
-		launch_pipeq2<FEAT, L16, false, true>(a, grid, dl, s);
-	else
-		launch_pipeq2<FEAT, L16, false, false>(a, grid, dl, s);
+		if constexpr ((FEAT & F_IPV6) != 0)
+			if (a.v6p) {
+				if (a.qt_live == 3 && a.v6p == 2)
+					launch_pipeq2<FEAT, L16, true, false, 2>(a, grid, dl, s);
+				else if (a.qt_live == 3)
+					launch_pipeq2<FEAT, L16, true, false, 1>(a, grid, dl, s);
+				else if (a.v6p == 2 && a.pwide)
+					launch_pipeq2<FEAT, L16, false, true, 2>(a, grid, dl, s);
+				else if (a.v6p == 2)
+					launch_pipeq2<FEAT, L16, false, false, 2>(a, grid, dl, s);
+				else if (a.pwide)
+					launch_pipeq2<FEAT, L16, false, true, 1>(a, grid, dl, s);
+				else
+					launch_pipeq2<FEAT, L16, false, false, 1>(a, grid, dl, s);
+				return;
+			}
+		if (a.qt_live == 3)
+			launch_pipeq2<FEAT, L16, true, false>(a, grid, dl, s);
+		else if (a.pwide)
+			launch_pipeq2<FEAT, L16, false, true>(a, grid, dl, s);
+		else
+			launch_pipeq2<FEAT, L16, false, false>(a, grid, dl, s);
+	}
 }
 
 template <uint32_t FEAT>
@@ -1784,6 +1799,57 @@ static int occupancy_cw(size_t dyn)
 	return m;
 }
 
+// Resident workgroups per CU of the quotient-index kernel (kind 5): the
+// fewest over the variants a launch may take -- both directions, the u32
+// log, the IPv6 lookups, the Ethernet key table: their LDS and registers
+// differ -- so the persistent grid and the hit-log slices sized from it hold
+// for whichever one runs.  (A program with Ethernet lookups runs the
+// instantiations without them unless the key table is live, launch_pipeq.)
+template <uint32_t FEAT>
+static int occupancy_qt(uint32_t window, size_t dyn, hipError_t &e)
+{
+	constexpr uint32_t G = FEAT & ~F_ETH;
+	int m = 0;
+	auto q = [&](const void *k, int thr) {
+		int x = 0;
+		const hipError_t r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k, thr, dyn);
+		if (r != hipSuccess)
+			e = r;
+		else if (x > 0 && (m == 0 || x < m))
+			m = x;
+	};
+	if (window <= 64) {
+		q((const void *)xfg_pipeq_kernel<G, 64, true, true, false, false, 0>, QT_THREADS(64));
+		q((const void *)xfg_pipeq_kernel<G, 64, true, true, true, false, 0>, QT_THREADS(64));
+		q((const void *)xfg_pipeq_kernel<G, 64, true, true, false, true, 0>, QT_THREADS(64));
+		if constexpr ((FEAT & F_IPV6) != 0) {
+			q((const void *)xfg_pipeq_kernel<G, 64, true, true, false, false, 1>, QT_THREADS(64));
+			q((const void *)xfg_pipeq_kernel<G, 64, true, true, false, true, 2>, QT_THREADS(64));
+			q((const void *)xfg_pipeq_kernel<G, 64, true, true, true, false, 2>, QT_THREADS(64));
+		}
+		if constexpr ((FEAT & F_ETH) != 0) {
+			q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, false, 0>, QT_THREADS(64));
+			q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, true, false, 0>, QT_THREADS(64));
+			q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, true, 0>, QT_THREADS(64));
+		}
+	} else {
+		q((const void *)xfg_pipeq_kernel<G, 128, false, true, false, false, 0>, QT_THREADS(128));
+		q((const void *)xfg_pipeq_kernel<G, 128, false, true, true, false, 0>, QT_THREADS(128));
+		q((const void *)xfg_pipeq_kernel<G, 128, false, true, false, true, 0>, QT_THREADS(128));
+		if constexpr ((FEAT & F_IPV6) != 0) {
+			q((const void *)xfg_pipeq_kernel<G, 128, false, true, false, false, 1>, QT_THREADS(128));
+			q((const void *)xfg_pipeq_kernel<G, 128, false, true, false, true, 2>, QT_THREADS(128));
+			q((const void *)xfg_pipeq_kernel<G, 128, false, true, true, false, 2>, QT_THREADS(128));
+		}
+		if constexpr ((FEAT & F_ETH) != 0) {
+			q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, false, 0>, QT_THREADS(128));
+			q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, true, false, 0>, QT_THREADS(128));
+			q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, true, 0>, QT_THREADS(128));
+		}
+	}
+	return m;
+}
+
 // Resident workgroups per CU of a classify kernel (persistent grid sizing)
 // with `dyn` bytes of dynamic LDS: kind 0 = general, 1 = pipelined (key
 // mode 0), 2 = pipelined (key mode 1), 5 = pipelined over the quotient
@@ -1796,7 +1862,7 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 	hipError_t e = hipSuccess;
 	bool done = false;
 	if (kind == 7)   // (the quotient-index kernel with its count wave, 64-byte windows)
-		return window <= 64 ? occupancy_cw<FEAT>(dyn) : 0;
+		return window <= 64 ? occupancy_cw<FEAT & ~F_ETH>(dyn) : 0;
 	if constexpr ((FEAT & F_IPV4) != 0) {
 #ifdef XFG_DIAG
 		if (kind == 3) {        // split: the lookup pass
@@ -1817,40 +1883,8 @@ static int occupancy_feat(int kind, uint32_t window, size_t dyn)
 				? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 64, true>, PIPE_THREADS(64), dyn)
 				: hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xfg_pipe4_kernel<FEAT, 128, false>, PIPE_THREADS(128), dyn);
 		} else if (kind == 5) {
-			// (the fewest over the variants a launch may take -- both
-			// directions, the u32 log, the IPv6 lookups: their LDS and
-			// registers differ -- so the persistent grid and the hit-log
-			// slices sized from it hold for whichever one runs)
 			done = true;
-			int m = 0;
-			auto q = [&](const void *k, int thr) {
-				int x = 0;
-				const hipError_t r = hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k, thr, dyn);
-				if (r != hipSuccess)
-					e = r;
-				else if (x > 0 && (m == 0 || x < m))
-					m = x;
-			};
-			if (window <= 64) {
-				q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, false, 0>, QT_THREADS(64));
-				q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, true, false, 0>, QT_THREADS(64));
-				q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, true, 0>, QT_THREADS(64));
-				if constexpr ((FEAT & F_IPV6) != 0) {
-					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, false, 1>, QT_THREADS(64));
-					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, false, true, 2>, QT_THREADS(64));
-					q((const void *)xfg_pipeq_kernel<FEAT, 64, true, true, true, false, 2>, QT_THREADS(64));
-				}
-			} else {
-				q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, false, 0>, QT_THREADS(128));
-				q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, true, false, 0>, QT_THREADS(128));
-				q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, true, 0>, QT_THREADS(128));
-				if constexpr ((FEAT & F_IPV6) != 0) {
-					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, false, 1>, QT_THREADS(128));
-					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, false, true, 2>, QT_THREADS(128));
-					q((const void *)xfg_pipeq_kernel<FEAT, 128, false, true, true, false, 2>, QT_THREADS(128));
-				}
-			}
-			n = m;
+			n = occupancy_qt<FEAT>(window, dyn, e);
 		}
 	}
 	if constexpr ((FEAT & F_ETH) != 0 && (FEAT & (F_IPV4 | F_IPV6 | F_TCP | F_UDP)) == 0) {

@@ -177,12 +177,13 @@ struct xfg_kargs {
 	 * the words read from memory */
 	uint32_t bl_lds;
 	uint32_t bl_off[3];
-	/* The Ethernet-key kernel (xdpfilt_{alw,dny}_eth; a map of at most
-	 * XFG_EK_MAX_KEYS keys whose flags agree on every device): the map as an
-	 * open-addressed table of ek_slots (a power of two) 16-byte entries
+	/* The Ethernet map as an LDS key table (a map of at most
+	 * XFG_EK_MAX_KEYS keys whose flags agree on every device; the
+	 * Ethernet-key kernel, the generic pipelined kernel, the index kernel):
+	 * an open-addressed table of ek_slots (a power of two) 16-byte entries
 	 * {MAC bytes 0-3, bytes 4-5, slot, flags | XFG_EK_VALID}, copied to LDS
 	 * by every workgroup; a key sits at most ek_disp entries past its home
-	 * (xfg_hash_eth & (ek_slots - 1)).  NULL: not this kernel. */
+	 * (xfg_ek_home with the map's seed).  NULL: no table. */
 	const uint32_t *ek;
 	uint32_t ek_slots;
 	uint32_t ek_disp;
@@ -316,6 +317,19 @@ XFG_HD uint32_t xfg_hash_eth(uint64_t mac, uint32_t seed)
 {
 	uint32_t h = xfg_fmix32((uint32_t)mac ^ seed);
 	return xfg_fmix32(h ^ (uint32_t)(mac >> 32));
+}
+
+/* The LDS key table's home entry of a MAC (lo: bytes 0-3, hi: bytes 4-5)
+ * in a table of 2^lg entries: multiply-shift over the MAC's two 24-bit
+ * halves, the top lg bits of the sum.  Only 24-bit multiplies (full rate on
+ * the vector ALU, where xfg_hash_eth's four 32-bit ones are quarter rate):
+ * every frame probes both of its MACs, so this is on the per-packet path. */
+XFG_HD uint32_t xfg_ek_home(uint32_t lo, uint32_t hi, uint32_t seed, uint32_t lg)
+{
+	const uint32_t a = (lo ^ seed) & 0xffffffu;
+	const uint32_t b = ((lo >> 24) | (hi << 8)) ^ (seed >> 8);
+	const uint32_t h = a * 0x9e3779u + (b & 0xffffffu) * 0x7f4a7bu;
+	return h >> (32 - lg);
 }
 
 XFG_HD uint32_t xfg_home(uint32_t h, uint32_t nbuckets)

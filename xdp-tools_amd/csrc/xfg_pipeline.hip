@@ -142,8 +142,7 @@ __device__ __forceinline__ u32x4 *ek_base(const xfg_kargs &a, uint32_t *s_dyn)
 __device__ __forceinline__ bool ek_probe(const u32x4 *s_ek, uint32_t es, uint32_t edisp, uint32_t seed,
 					 uint32_t lo, uint32_t hi, uint32_t mask, uint32_t &slot)
 {
-	const uint32_t h = xfg_hash_eth(lo | ((uint64_t)hi << 32), seed);
-	uint32_t e = h & (es - 1);
+	uint32_t e = xfg_ek_home(lo, hi, seed, __builtin_ctz(es));
 	bool hit = false;
 	for (uint32_t d = 0; d <= edisp; d++) {
 		const u32x4 v = s_ek[e];

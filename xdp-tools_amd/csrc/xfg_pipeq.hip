@@ -439,6 +439,19 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	const uint32_t *s_ports = stage_ports<FEAT>(a, s_tab, s_dyn, tid, NT);
 	const bool ptab = PORTS && a.port_count && a.port_tab;
 	const uint32_t pdisp = rfl(a.port_tab_disp), gb3 = rfl(a.gbase[3]);
+	// (ekon: live Ethernet keys beside the index, the Ethernet map as its
+	// LDS key table -- lookup_verdict_ethernet answered in LDS before the
+	// IP lookups, xdpfilt_prog.h:187-196,224-227; a hit ends the program)
+	constexpr bool EKF = (FEAT & F_ETH) != 0;
+	const bool ekon = EKF && a.ek != nullptr;
+	const uint32_t ek_es = EKF ? rfl(a.ek_slots) : 0u, ek_disp = EKF ? rfl(a.ek_disp) : 0u;
+	const uint32_t ek_seed = EKF ? rfl(a.te.seed) : 0u, ek_gb = EKF ? rfl(a.gbase[2]) : 0u;
+	const bool ek_dl = ekon && can_hit(a.te.fmask, M_DST), ek_sl = ekon && can_hit(a.te.fmask, M_SRC);
+	u32x4 *const s_ek = ek_base(a, s_dyn);
+	if constexpr (EKF)
+		if (ekon)
+			for (uint32_t i = tid; i < ek_es; i += NT)
+				s_ek[i] = reinterpret_cast<const u32x4 *>(a.ek)[i];
 	if constexpr (PORTS)
 		for (int i = tid; i < (int)(XFG_PORT_TAB + XL); i += NT)
 			s_pcnt[i] = 0;
@@ -1014,12 +1027,35 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 			else
 				r = parse_bf<FEAT, W>(myrow, len);
 			const bool valid = gi < n;
+			// (ekon) the Ethernet lookups: dst MAC then src MAC against the
+			// LDS table, for a frame past parse_ethhdr (14 bytes); a frame
+			// the parse defers is walked whole, its MACs with it
+			bool ekh = false;
+			uint32_t ekt = CT_NONE;
+			if constexpr (EKF) {
+				if (ekon) {
+					uint32_t sl = 0;
+					bool h = false;
+					if (ek_dl)
+						h = ek_probe(s_ek, ek_es, ek_disp, ek_seed, dw[0], dw[1] & 0xffffu, M_DST, sl);
+					if (ek_sl) {
+						uint32_t s2 = 0;
+						const bool h2 = ek_probe(s_ek, ek_es, ek_disp, ek_seed,
+									 __builtin_amdgcn_alignbyte(dw[2], dw[1], 2), dw[2] >> 16,
+									 M_SRC, s2);
+						sl = h ? sl : s2;
+						h |= h2;
+					}
+					ekh = valid & (len >= 14) & !r.defer & h;
+					ekt = ek_gb + sl;
+				}
+			}
 			bool def6 = false;
 			if constexpr (V6P) {
 				// the IPv6 key (daddr at 38, saddr at 22: two bytes into a
 				// row dword), its home bucket, its rank among the tile's
 				// lookups; ranks below 16 post their bucket for L6
-				const bool k6 = valid & !r.defer & r.v6ok & k6live;
+				const bool k6 = valid & !r.defer & r.v6ok & k6live & !ekh;
 				uint32_t w6[4], ws[4];
 #pragma unroll
 				for (int i = 0; i < 4; i++) {
@@ -1056,7 +1092,7 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 			}
 			// (IPv6 keys live without V6P: every IPv6 frame deferred)
 			const bool rdef = r.defer | (v6d & r.is6 & !V6P) | def6;
-			const bool kok = valid & !rdef & r.v4ok & klive;
+			const bool kok = valid & !rdef & r.v4ok & klive & !ekh;
 			const uint32_t h = hk;
 			rs.b = pick(kok, h >> rsh, 0u);   // (no lookup: bucket 0, a shared line)
 			rs.key = XFG_QT_USED | (h & rmask);
@@ -1091,6 +1127,9 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 					fa = pick(ph, HIT, fa);
 				}
 			}
+			fa = pick(ekh, HIT, fa);
+			fs = pick(ekh, XFG_PORT_TAB, fs);
+			ft = pick(ekh, ekt, ft);
 			rs.pk = pk3(pick(!valid, A_NONE, pick(rdef, A_DEFER, fa)),
 				   pick(valid & !rdef, fs, XFG_PORT_TAB), len);
 			rs.tag = pick(valid & !rdef, ft, CT_NONE);
