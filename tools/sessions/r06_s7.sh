@@ -3,7 +3,7 @@
 # cheaper home function (24-bit multiplies): Ethernet and index-kernel
 # tests, C1 / C3e / C3 / C2, the bench line.
 R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out; mkdir -p $OUT; export PYTHONUNBUFFERED=1
-T=s7
+T=${T:-s7}
 step() {
 	local t=$1; shift
 	timeout -k 10 "$t" "$@"

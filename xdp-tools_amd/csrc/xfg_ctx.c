@@ -2552,7 +2552,12 @@ static int host_registered(xfg_ctx *ctx, const void *p, uint64_t bytes, const ui
 #define HYB_ZC_CH (1ull << 20)
 #endif
 #ifndef HYB_ST_N    /* ... and its staged chunks of HOST_CH (0: no hybrid) */
-#define HYB_ST_N 2u
+/* (off: on C5 from a registered buffer, 2^23 frames of 1514 B, zero copy
+ * alone ran 270 Mpps and every hybrid setting tried 175-220 -- the staged
+ * gather's reads of the same host memory slow the kernels' PCIe reads more
+ * than its chunks add, profiles/r06_s6_hyb_c5.log; the diagnostics build
+ * still takes XFG_HYB_ZLOG2 / XFG_HYB_ST) */
+#define HYB_ST_N 0u
 #endif
 _Static_assert((size_t)ZC_CH * 13 + 256 <= (size_t)HOST_CH * HOST_WIN, "slot buffers hold a chunk");
 _Static_assert((size_t)ZC_CH * 2 * 5 + 256 <= (size_t)HOST_CH * HOST_WIN, "slot buffers hold a chunk");
@@ -2723,7 +2728,7 @@ static int host_run(xfg_ctx *ctx, int dev, const struct hsrc *src, uint64_t n, u
 	if ((err = host_staging(d)))
 		goto fail;
 	/* (registered large slots, a batch of several rounds: zero copy and the
-	 * staged gather side by side, host_run_hyb) */
+	 * staged gather side by side, host_run_hyb -- off by default, HYB_ST_N) */
 	uint64_t hyb_zc = HYB_ZC_CH;
 	uint32_t hyb_st = HYB_ST_N;
 #ifdef XFG_DIAG

@@ -48,24 +48,24 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 	constexpr int NW = EK_WAVES, NT = EK_THREADS, G = XFG_EK_G, D = XFG_EK_D;
 	constexpr uint32_t HIT = (FEAT & F_DENY) ? A_PASS : A_DROP;
 	constexpr uint32_t MISS = (FEAT & F_DENY) ? A_DROP : A_PASS;
-	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES];
+	__shared__ uint32_t s_ecnt[XFG_EK_SLOTS_MAX];   // hits per key-table entry
 	__shared__ unsigned long long s_stats[6];
 	extern __shared__ uint32_t s_dyn[];
 
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-	Counters cn{ s_ctag, s_ccnt, dcnt_base(a, s_dyn) };
-	cn.init(a, tid, NT);
 	if (tid < 6)
 		s_stats[tid] = 0;
 	const uint32_t es = rfl(a.ek_slots), edisp = rfl(a.ek_disp);
 	u32x4 *const s_ek = ek_base(a, s_dyn);
-	for (uint32_t i = tid; i < es; i += NT)
+	for (uint32_t i = tid; i < es; i += NT) {
 		s_ek[i] = reinterpret_cast<const u32x4 *>(a.ek)[i];
+		s_ecnt[i] = 0;
+	}
 	// live lookups (flag census): dst, then src (xdpfilt_prog.h:187-196)
 	const bool dlive = a.te.count && can_hit(a.te.fmask, M_DST);
 	const bool slive = a.te.count && can_hit(a.te.fmask, M_SRC);
-	const uint32_t seed = rfl(a.te.seed), gbe = rfl(a.gbase[2]), lg_lo = rfl(a.dcnt);
+	const uint32_t seed = rfl(a.te.seed), gbe = rfl(a.gbase[2]);
 	__syncthreads();
 
 	const uint32_t n = (uint32_t)a.n, nt = (n + 63) / 64;
@@ -75,14 +75,6 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 	const uint64_t stride = a.stride;
 	const uint8_t *const lens = static_cast<const uint8_t *>(a.lens);
 
-	// a hit's counter: its direct LDS counter, else the LDS counter cache
-	// (C1's eight hot keys merge there) and atomics
-	auto count = [&](uint32_t tag) {
-		const bool dc = tag < lg_lo;
-		if (dc)
-			atomicAdd(&cn.dcnt[tag], 1u);
-		cn.bump(a, dc ? CT_NONE : tag, lane);
-	};
 	// per-action packets (wave totals) and bytes (per lane)
 	uint32_t st_c0 = 0, st_c1 = 0, st_c2 = 0, st_b0 = 0, st_b1 = 0, st_b2 = 0;
 	auto stat = [&](bool valid, uint32_t act, uint32_t len) {
@@ -94,11 +86,13 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 		st_b2 += (valid & (act == A_PASS)) ? len : 0u;
 	};
 	// CHECK_MAP (xdpfilt_prog.h:56-64) against the LDS table: the key found
-	// with every bit of mask set.  Every lane reads edisp + 1 entries from
-	// its home (a key sits at most that far past it; keys are unique, so at
-	// most one entry matches).
-	auto probe = [&](uint32_t lo, uint32_t hi, uint32_t mask, uint32_t &slot) {
-		return ek_probe(s_ek, es, edisp, seed, lo, hi, mask, slot);
+	// with every bit of mask set, the entry it sits in.  Every lane reads
+	// edisp + 1 entries from its home (a key sits at most that far past it;
+	// keys are unique, so at most one entry matches).  A hit counts on its
+	// entry's LDS counter (one LDS atomic, whatever the keys' heat), added to
+	// the key's counter once per workgroup.
+	auto probe = [&](uint32_t lo, uint32_t hi, uint32_t mask, uint32_t &ent) {
+		return ek_probe<true>(s_ek, es, edisp, seed, lo, hi, mask, ent);
 	};
 
 	// a group's first 16 bytes and lengths (tiles past the wave's share and
@@ -136,7 +130,8 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 			const uint32_t act = !look ? A_ABORTED : (hd | hs) ? HIT : MISS;
 			if (valid)
 				__builtin_nontemporal_store((uint8_t)act, a.verdicts + gi);
-			count(hd ? gbe + sd : hs ? gbe + ss : CT_NONE);
+			if (hd | hs)
+				atomicAdd(&s_ecnt[hd ? sd : ss], 1u);
 			stat(valid, act, len);
 		}
 	};
@@ -178,7 +173,9 @@ __global__ __launch_bounds__(EK_THREADS, XFG_EK_MINW) void xfg_pipee_kernel(cons
 	__syncthreads();
 	if (tid < 6 && s_stats[tid])
 		atomicAdd(&a.stats[tid], s_stats[tid]);
-	cn.flush(a, tid, NT);
+	for (uint32_t i = tid; i < es; i += NT)
+		if (const uint32_t c = s_ecnt[i])
+			atomicAdd(global_counter(a, gbe + s_ek[i].z), (unsigned long long)c);
 }
 
 }  // namespace

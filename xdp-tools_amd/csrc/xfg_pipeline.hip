@@ -137,8 +137,9 @@ __device__ __forceinline__ u32x4 *ek_base(const xfg_kargs &a, uint32_t *s_dyn)
 
 // CHECK_MAP (xdpfilt_prog.h:56-64) of one MAC against the LDS key table
 // (es entries, keys at most edisp past their home): found with every bit of
-// mask set; its canonical slot.  Every lane reads edisp + 1 entries (keys
-// are unique: at most one matches).
+// mask set; its canonical slot (ENTRY: the table entry it sits in).  Every
+// lane reads edisp + 1 entries (keys are unique: at most one matches).
+template <bool ENTRY = false>
 __device__ __forceinline__ bool ek_probe(const u32x4 *s_ek, uint32_t es, uint32_t edisp, uint32_t seed,
 					 uint32_t lo, uint32_t hi, uint32_t mask, uint32_t &slot)
 {
@@ -148,7 +149,7 @@ __device__ __forceinline__ bool ek_probe(const u32x4 *s_ek, uint32_t es, uint32_
 		const u32x4 v = s_ek[e];
 		const bool m = (v.x == lo) & (v.y == hi) & ((v.w & XFG_EK_VALID) != 0);
 		hit |= m & ((v.w & mask) == mask);
-		slot = m ? v.z : slot;
+		slot = m ? (ENTRY ? e : v.z) : slot;
 		e = (e + 1) & (es - 1);
 	}
 	return hit;

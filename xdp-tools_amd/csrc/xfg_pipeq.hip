@@ -302,7 +302,13 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	__shared__ uint32_t s_res[XFG_LOG_PARTS + XL];
 	__shared__ __attribute__((aligned(8))) uint32_t s_hd[2 * (XFG_LOG_PARTS + XL)];
 	__shared__ uint32_t s_tab[PORTS ? XFG_PORT_TAB : 1];
-	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB + XL : 1];
+	// (EKF: past the ports' counters and the lanes' words, one a key-table
+	// entry -- a live Ethernet key's hits, flushed once per workgroup)
+	constexpr bool EKF = (FEAT & F_ETH) != 0;
+	constexpr uint32_t EKC = EKF ? XFG_EK_SLOTS_MAX : 0u;
+	static_assert(!EKF || PORTS, "the Ethernet lookups count beside the ports");
+	static_assert(XFG_PORT_TAB + XL + EKC <= 0x1000u, "a counter slot fits its 12 bits");
+	__shared__ uint32_t s_pcnt[PORTS ? XFG_PORT_TAB + XL + EKC : 1];
 	__shared__ uint32_t s_ctag[CC_ENTRIES], s_ccnt[CC_ENTRIES], s_tn[NW];
 	__shared__ uint32_t s_lh[XFG_LOG_PARTS];
 	__shared__ unsigned long long s_stats[6];
@@ -442,7 +448,6 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	// (ekon: live Ethernet keys beside the index, the Ethernet map as its
 	// LDS key table -- lookup_verdict_ethernet answered in LDS before the
 	// IP lookups, xdpfilt_prog.h:187-196,224-227; a hit ends the program)
-	constexpr bool EKF = (FEAT & F_ETH) != 0;
 	const bool ekon = EKF && a.ek != nullptr;
 	const uint32_t ek_es = EKF ? rfl(a.ek_slots) : 0u, ek_disp = EKF ? rfl(a.ek_disp) : 0u;
 	const uint32_t ek_seed = EKF ? rfl(a.te.seed) : 0u, ek_gb = EKF ? rfl(a.gbase[2]) : 0u;
@@ -453,7 +458,7 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 			for (uint32_t i = tid; i < ek_es; i += NT)
 				s_ek[i] = reinterpret_cast<const u32x4 *>(a.ek)[i];
 	if constexpr (PORTS)
-		for (int i = tid; i < (int)(XFG_PORT_TAB + XL); i += NT)
+		for (int i = tid; i < (int)(XFG_PORT_TAB + XL + EKC); i += NT)
 			s_pcnt[i] = 0;
 	for (int i = tid; i < (int)XFG_LOG_PARTS; i += NT)
 		s_lh[i] = 0;
@@ -485,7 +490,7 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	// through Counters::bump
 	auto count = [&](uint32_t tag, uint32_t pslot) {
 		const bool q = (tag != CT_NONE) & ((tag & QTAG) != 0);
-		const bool ps = pslot < XFG_PORT_TAB;
+		const bool ps = pslot != XFG_PORT_TAB;   // (a port's table slot, or EKF a key-table entry's)
 		const bool dc = !q & (tag < a.dcnt);
 		const uint32_t qs = tag & ~QTAG;
 		if constexpr (XFG_QT_CNT2) {
@@ -1031,23 +1036,23 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 			// LDS table, for a frame past parse_ethhdr (14 bytes); a frame
 			// the parse defers is walked whole, its MACs with it
 			bool ekh = false;
-			uint32_t ekt = CT_NONE;
+			uint32_t eke = 0;
 			if constexpr (EKF) {
 				if (ekon) {
 					uint32_t sl = 0;
 					bool h = false;
 					if (ek_dl)
-						h = ek_probe(s_ek, ek_es, ek_disp, ek_seed, dw[0], dw[1] & 0xffffu, M_DST, sl);
+						h = ek_probe<true>(s_ek, ek_es, ek_disp, ek_seed, dw[0], dw[1] & 0xffffu, M_DST, sl);
 					if (ek_sl) {
 						uint32_t s2 = 0;
-						const bool h2 = ek_probe(s_ek, ek_es, ek_disp, ek_seed,
-									 __builtin_amdgcn_alignbyte(dw[2], dw[1], 2), dw[2] >> 16,
-									 M_SRC, s2);
+						const bool h2 = ek_probe<true>(s_ek, ek_es, ek_disp, ek_seed,
+									       __builtin_amdgcn_alignbyte(dw[2], dw[1], 2),
+									       dw[2] >> 16, M_SRC, s2);
 						sl = h ? sl : s2;
 						h |= h2;
 					}
 					ekh = valid & (len >= 14) & !r.defer & h;
-					ekt = ek_gb + sl;
+					eke = XFG_PORT_TAB + XL + sl;   // (the entry's LDS counter)
 				}
 			}
 			bool def6 = false;
@@ -1128,8 +1133,8 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 				}
 			}
 			fa = pick(ekh, HIT, fa);
-			fs = pick(ekh, XFG_PORT_TAB, fs);
-			ft = pick(ekh, ekt, ft);
+			fs = pick(ekh, eke, fs);
+			ft = pick(ekh, CT_NONE, ft);
 			rs.pk = pk3(pick(!valid, A_NONE, pick(rdef, A_DEFER, fa)),
 				   pick(valid & !rdef, fs, XFG_PORT_TAB), len);
 			rs.tag = pick(valid & !rdef, ft, CT_NONE);
@@ -1317,6 +1322,11 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 			for (int i = tid; i < (int)XFG_PORT_TAB; i += NT)
 				if (s_pcnt[i])
 					atomicAdd(a.port_hits + (s_tab[i] & 0xffff), (unsigned long long)s_pcnt[i]);
+	if constexpr (EKF)
+		if (ekon)
+			for (uint32_t i = tid; i < ek_es; i += NT)
+				if (const uint32_t c = s_pcnt[XFG_PORT_TAB + XL + i])
+					atomicAdd(global_counter(a, ek_gb + s_ek[i].z), (unsigned long long)c);
 	if (dg & 16)
 		return;
 }
