@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "xdp-tools_amd", "python"))
 import bench  # noqa: E402
 
 KNOBS = ("XFG_KERNEL", "XFG_COUNT", "XFG_EMPTY", "XFG_GRID_PER_CU", "XFG_DIAG_MASK", "XFG_QT", "XFG_LOG_PEND",
-         "XFG_BLOOM_LDS", "XFG_CW", "XFG_CW_LOG_MIN")
+         "XFG_BLOOM_LDS", "XFG_CW", "XFG_CW_LOG_MIN", "XFG_QT_DYN_MIN")
 
 
 def main():

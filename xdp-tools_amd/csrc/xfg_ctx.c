@@ -1599,6 +1599,9 @@ static int fill_kargs(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_batch *b
 	const char *dm = getenv("XFG_DIAG_MASK");   /* pipelined IPv4-key kernel: drop a cost */
 	if (dm && *dm)
 		a->diag = (uint32_t)strtoul(dm, NULL, 0);
+	const char *tsp = getenv("XFG_TSTAMP");   /* device buffer for the QT kernel's phase stamps */
+	if (tsp && *tsp)
+		a->tstamp = (unsigned long long *)(uintptr_t)strtoull(tsp, NULL, 0);
 	const char *kk = getenv("XFG_KERNEL");   /* "split": parse + lookup passes */
 	if (kk && !strcmp(kk, "split"))
 		a->split = a->pipe && a->km;
@@ -1861,9 +1864,13 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 		a.rec_kb = both ? d->rec + 2 * a.n : NULL;
 	}
 	if (a.pipe && !ek_only) {   /* (the Ethernet-key kernel defers nothing) */
-		/* one deferred list per wave, room for every packet of its tiles */
+		/* one deferred list per wave, room for every packet of its tiles --
+		 * a quarter more than a fixed share: the quotient-index kernel's
+		 * waves take their workgroup's tiles as they go (XFG_QT_DYN), at
+		 * most defer_cap / 64 each */
 		uint64_t nw = grid * (per_wg / 64), nt = (a.n + 63) / 64;
-		uint64_t cap = (nt + nw - 1) / nw * 64;
+		uint64_t per = (nt + nw - 1) / nw;
+		uint64_t cap = (per + per / 4 + 2) * 64;
 		if ((err = scratch(d, (void **)&d->defer, &d->defer_bytes, nw * cap * 4)))
 			goto out;
 		a.defer = d->defer;
@@ -1911,7 +1918,10 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 			 grid <= XFG_LOG_SLICES_MAX;
 	/* slice (partition, workgroup): twice a uniform share of the most the
 	 * workgroup's waves can log (a fuller one spills) */
-	const uint64_t wg_max = (per_wg / 64) * (uint64_t)a.defer_cap;
+	/* (a workgroup's tiles are a fixed share whichever of its waves takes
+	 * them: the share, not the deferred lists' room) */
+	const uint64_t wg_nw = per_wg / 64, wg_all = grid * wg_nw;
+	const uint64_t wg_max = wg_nw * (((a.n + 63) / 64 + wg_all - 1) / wg_all) * 64;
 	const uint64_t pcap = (2 * ((wg_max + XFG_LOG_PARTS - 1) / XFG_LOG_PARTS) + 64 + 7) & ~7ull;
 	/* the quotient-index kernel's logs of up to K launches side by side in
 	 * the partition buffers, counted by one count kernel (its fixed cost
@@ -1949,6 +1959,17 @@ static int launch_batch(xfg_ctx *ctx, struct xfg_dev *d, const struct xfg_kargs 
 #endif
 	if (cw)
 		K = 2;
+	/* (the QT kernel's waves taking their workgroup's tiles as they go,
+	 * C3 on one box: 2^26 1.059-1.061 against 1.089-1.092 ms, 2^24
+	 * 0.294-0.296 against 0.304-0.306, 2^21 equal; C4 at 2^21 1.5 % slower
+	 * -- profiles/r06_s13_session.log) */
+	uint64_t dyn_min = XFG_QT_DYN_MIN;
+#ifdef XFG_DIAG
+	const char *dme = getenv("XFG_QT_DYN_MIN");   /* packets from which they do */
+	if (dme && *dme)
+		dyn_min = strtoull(dme, NULL, 0);
+#endif
+	a.qt_dyn = a.qt && a.n >= dyn_min;
 	/* logs pending from earlier launches: counted first unless this one
 	 * appends to them -- or, in the count wave's mode, counts them (the
 	 * same shape, the same counts) */

@@ -104,6 +104,7 @@
 #define XFG_CW_HIST_MAX   8192u   /* the QT kernel's count-wave histogram entries (32 KiB) */
 #define XFG_CW_LOG_MIN    (1ull << 20)   /* packets from which the count wave's log runs */
 #define XFG_CW_MAX_PACKETS (1ull << 25)   /* ... and below which it does */
+#define XFG_QT_DYN_MIN    (1ull << 23)   /* packets from which the QT waves take tiles as they go */
 #define XFG_LOG_PASSES_MAX 32u    /* histogram passes per partition (span 512K) */
 #define XFG_LOG_SLICES_MAX 1024u  /* slices per partition: classify workgroups */
 #define XFG_DEFER_SRC_MAX 4096u   /* deferred lists (classify waves) xfg_defer_kernel takes */
@@ -224,6 +225,12 @@ struct xfg_kargs {
 	uint32_t defer_sep;
 	uint32_t defer_grid;
 	uint32_t diag;                /* diagnostics build only (XFG_DIAG_MASK); 0 */
+	/* diagnostics build only (XFG_TSTAMP): the quotient-index kernel's phase
+	 * times, 32 wall-clock stamps a workgroup (xfg_pipeq.hip QT_STAMP); NULL */
+	unsigned long long *tstamp;
+	/* quotient-index kernel: a workgroup's waves take its tiles from an LDS
+	 * counter (XFG_QT_DYN) -- batches of at least XFG_QT_DYN_MIN packets */
+	uint32_t qt_dyn;
 	/* Header-window batches (xfg_classify_host): each slot holds only the
 	 * first `stride` bytes of its frame, lens are the frames' true lengths.
 	 * A packet whose program reads past the window is not classified here:

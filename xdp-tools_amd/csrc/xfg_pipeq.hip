@@ -95,6 +95,9 @@
 #ifndef XFG_QT_PLIP      /* 1: the bucket halves swapped in place by inline asm */
 #define XFG_QT_PLIP 0
 #endif
+#ifndef XFG_QT_DYN       /* 1: a workgroup's waves take its tiles from an LDS counter (0: a fixed share each) */
+#define XFG_QT_DYN 1
+#endif
 #ifndef XFG_QT_PADV      /* (A/B only: extra VALU / SALU instructions per tile, to price one) */
 #define XFG_QT_PADV 0
 #endif
@@ -334,6 +337,20 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	constexpr uint32_t dg = 0;
 #endif
 	const int tid = threadIdx.x, lane = tid & 63;
+	// (diagnostics: phase stamps, 32 a workgroup -- 0 entry, 1 set-up done,
+	// 2 + w wave w's loop done (10: the count wave's), 11 + w its deferred
+	// walk done, 20 the partitions moved, 21 wave 0's end)
+#ifdef XFG_DIAG
+#define QT_STAMP(slot)                                                                        \
+	do {                                                                                  \
+		if (a.tstamp && lane == 0)                                                    \
+			a.tstamp[(uint64_t)blockIdx.x * 32 + (slot)] = wall_clock64();        \
+	} while (0)
+#else
+#define QT_STAMP(slot) do { } while (0)
+#endif
+	if (tid == 0)
+		QT_STAMP(0);
 	auto piece = [&](int it, uint32_t &pk, uint32_t &sub) {
 		const uint32_t c = it * 64 + (uint32_t)lane;
 		pk = SWZ ? it * 16 + ((uint32_t)lane >> 5) * 8 + ((uint32_t)lane & 7) : c / CPP;
@@ -372,6 +389,16 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	auto tileOf = [&](uint32_t kk) -> uint32_t {
 		return G == 1 ? first + kk * step : (first + (kk / G) * step) * G + (kk % G);
 	};
+	// (DYN: the workgroup's tiles -- round r holds tiles blockIdx.x * NW + j
+	// + r * step, j < NW -- taken by its waves from an LDS counter: each wave
+	// its own tile of rounds 0..D, loaded before the set-up as in the fixed
+	// share, then the next free one for every later iteration, taken an
+	// iteration before its windows are loaded.  Waves that share a SIMD do
+	// not progress alike: with a fixed share the workgroup's first wave
+	// ended its loop ~90 us before its last at 2^26, tools/qt_phases.py.  A
+	// wave takes at most defer_cap / 64 tiles, its deferred list's room.)
+	constexpr bool DYN = XFG_QT_DYN && G == 1;
+	__shared__ uint32_t s_next;
 	// windows + lengths of tile t (clamped to the last tile): CPP + 1 loads,
 	// always issued
 	// (the length width is a template parameter: one load of a fixed kind,
@@ -442,6 +469,8 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	cn.init(a, tid, NT);
 	if (tid < 6)
 		s_stats[tid] = 0;
+	if (DYN && tid == 0)
+		s_next = (D + 1) * NW;
 	const uint32_t *s_ports = stage_ports<FEAT>(a, s_tab, s_dyn, tid, NT);
 	const bool ptab = PORTS && a.port_count && a.port_tab;
 	const uint32_t pdisp = rfl(a.port_tab_disp), gb3 = rfl(a.gbase[3]);
@@ -708,10 +737,48 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	};
 	// (wcf: this iteration moves completed hit-log chunks -- every other one:
 	// a ring of WR entries takes two iterations' hits with room to spare)
+	// (one more with both directions: the last tile's src lookup resolves
+	// an iteration after its dst lookup)
+	const uint32_t nrun = (nt + G - 1) / G;
+	uint32_t iters = first < nrun ? ((nrun - 1 - first) / step + 1) * G + LAG + (R2 ? 1 : 0) : 0u;
+	// (DYN) tiles k - LAG - 1 .. k + D of iteration k (past the ends: nt);
+	// tiles this wave has taken, the most it may; whether more may follow
+	constexpr uint32_t RN = DYN ? LAG + D + 2 : 1;
+	uint32_t tr[RN];
+	uint32_t tmine = 0, tmax = 0;
+	bool more = false;
+	// (the host's choice per launch, kargs.qt_dyn: large batches; a fixed
+	// share otherwise -- tile k + D + 1 then follows from k)
+	const bool dyn_on = DYN && a.qt_dyn != 0;
+	if constexpr (DYN) {
+		tmax = rfl(a.defer_cap) / 64;
+#pragma unroll
+		for (uint32_t i = 0; i < RN; i++)
+			tr[i] = nt;
+#pragma unroll
+		for (uint32_t d = 0; d <= D; d++) {
+			const uint32_t t = first + d * step;
+			tr[LAG + 1 + d] = t < nt ? t : nt;
+			tmine += t < nt ? 1u : 0u;
+		}
+		more = dyn_on && tmine == D + 1;
+		if (dyn_on)
+			iters = more ? 0xffffffffu : tmine ? tmine + LAG + (R2 ? 1u : 0u) : 0u;
+	}
 	auto iteration = [&](uint32_t k, u32x4 (&cur)[CPP], len_t &curlen, RSt &rs, bool wcf) __attribute__((always_inline)) {
-		const uint32_t tP = tileOf(k);
+		// (DYN) tile k + D + 1, taken now from the counter and read at the
+		// iteration's end (the atomic's return waited for with the
+		// iteration's own LDS work): its windows are loaded next iteration;
+		// none left (or no room left in this wave's list): the loop ends once
+		// the tiles taken have drained through W
+		uint32_t graw = 0xffffffffu;
+		const bool take = DYN && more && tmine < tmax;
+		if constexpr (DYN)
+			if (take && lane == 0)
+				graw = atomicAdd(&s_next, 1u);
+		const uint32_t tP = DYN ? tr[LAG + 1] : tileOf(k);
 		const bool vP = tP < nt;
-		const uint32_t tR = k >= LAG ? tileOf(k - LAG) : nt;
+		const uint32_t tR = DYN ? tr[1] : k >= LAG ? tileOf(k - LAG) : nt;
 		const bool vR = tR < nt;
 		// everything but the newest iteration's loads (LAG 1: tile k+1's
 		// windows; LAG 2: also the last iteration's bucket loads; depth 3:
@@ -737,7 +804,7 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 		// (both directions: W works on tile k-2, whose src lookup -- read
 		// last iteration for the packets whose dst lookup decided nothing --
 		// R2 resolves first; one directions: W works on tile k-1)
-		const uint32_t tW = R2 ? (k >= LAG + 1 ? tileOf(k - LAG - 1) : nt) : tR;
+		const uint32_t tW = R2 ? (DYN ? tr[0] : k >= LAG + 1 ? tileOf(k - LAG - 1) : nt) : tR;
 		const bool vW = tW < nt;
 		if constexpr (R2) {
 			PMARK("R2");
@@ -1166,14 +1233,33 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 		// (issued before the parse instead, the compiler's register
 		// reuse puts waits into R: not kept)
 		__builtin_amdgcn_sched_barrier(0);
-		issue(tileOf(k + D), cur, curlen);
+		issue(DYN ? tr[LAG + 1 + D] : tileOf(k + D), cur, curlen);
 		__builtin_amdgcn_sched_barrier(0);
+		if constexpr (DYN) {
+			uint32_t nx = nt;
+			if (dyn_on) {
+				if (more) {
+					const uint32_t g = rfl(graw);
+					const uint32_t t = take ? blockIdx.x * NW + g % NW + g / NW * step : nt;
+					if (t < nt) {
+						nx = t;
+						tmine++;
+					} else {
+						more = false;
+						iters = k + D + 1 + LAG + (R2 ? 1u : 0u);
+					}
+				}
+			} else {
+				const uint32_t t = first + (k + D + 1) * step;
+				nx = t < nt ? t : nt;
+			}
+#pragma unroll
+			for (uint32_t i = 0; i + 1 < RN; i++)
+				tr[i] = tr[i + 1];
+			tr[RN - 1] = nx;
+		}
 	};
 
-	// (one more with both directions: the last tile's src lookup resolves
-	// an iteration after its dst lookup)
-	const uint32_t nrun = (nt + G - 1) / G;
-	const uint32_t iters = first < nrun ? ((nrun - 1 - first) / step + 1) * G + LAG + (R2 ? 1 : 0) : 0u;
 	// iteration k uses window buffer k % D and state set k % LAG: the loop
 	// body is U = lcm(D, LAG) iterations
 	constexpr uint32_t U = D == 3 ? 3 * LAG : 2;
@@ -1187,6 +1273,8 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 		else if constexpr (D == 3)
 			iteration(k, preC, lenC, rs, u % 2 == 0);
 	};
+	if (tid == 0)
+		QT_STAMP(1);
 	if (cwv) {
 		if constexpr (CW)   // (past the direct counters: the histogram)
 			qt_count_wave(a, (lds_u32 *)(dcnt_base(a, s_dyn) + ((a.dcnt + 3) & ~3u)));
@@ -1227,6 +1315,7 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 		}
 	}
 
+	QT_STAMP(2 + wv);
 	if constexpr (XFG_QT_VST)
 		if (vs_act <= A_PASS)
 			__builtin_nontemporal_store((uint8_t)vs_act, a.verdicts + vs_gi);
@@ -1250,6 +1339,7 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 		stat(act, len);
 	}
 
+	QT_STAMP(11 + wv);
 	st_fold();
 #pragma unroll
 	for (int kk = 0; kk < 3; kk++) {
@@ -1312,6 +1402,8 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 			gst32(a.pfill + (uint64_t)wc_p * a.pslices + a.pslice0 + blockIdx.x, hd);
 	}
 	__syncthreads();
+	if (tid == 0)
+		QT_STAMP(20);
 	if (cwv)
 		return;
 	if (tid < 6 && s_stats[tid])
@@ -1327,6 +1419,8 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 			for (uint32_t i = tid; i < ek_es; i += NT)
 				if (const uint32_t c = s_pcnt[XFG_PORT_TAB + XL + i])
 					atomicAdd(global_counter(a, ek_gb + s_ek[i].z), (unsigned long long)c);
+	if (tid == 0)
+		QT_STAMP(21);
 	if (dg & 16)
 		return;
 }
