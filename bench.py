@@ -48,7 +48,7 @@ KERNEL_OF_PATH = {
 # tools/pmc_summary.py): per launch path, the file and the batch it was taken at
 # (round 5: the QT kernel with pending logs and the mask-free rings; a pass of an
 # older kernel would misstate this one's traffic)
-PMC_OF_PATH = {5: ("profiles/archive/r05_c3_pmc_2p26.json", 1 << 26)}
+PMC_OF_PATH = {5: ("profiles/r06_c3_pmc_2p26.json", 1 << 26)}
 
 
 def committed_traffic(path, n, stream_bytes):

@@ -396,8 +396,11 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	// iteration before its windows are loaded.  Waves that share a SIMD do
 	// not progress alike: with a fixed share the workgroup's first wave
 	// ended its loop ~90 us before its last at 2^26, tools/qt_phases.py.  A
-	// wave takes at most defer_cap / 64 tiles, its deferred list's room.)
-	constexpr bool DYN = XFG_QT_DYN && G == 1;
+	// wave takes at most defer_cap / 64 tiles, its deferred list's room.
+	// Not with the Ethernet key table: its state beside the table's took
+	// C3e from 0.320 to 0.355 ms at 2^24, dynamic or not -- scalar
+	// registers spilled; r06_s8 / r06_s14_session.log)
+	constexpr bool DYN = XFG_QT_DYN && G == 1 && !EKF;
 	__shared__ uint32_t s_next;
 	// windows + lengths of tile t (clamped to the last tile): CPP + 1 loads,
 	// always issued
