@@ -65,6 +65,9 @@ def main():
             "count_wave": rel[:, 10] - rel[:, 1],
             "defer_walk": np.nanmax(dfr - loop, 1),
             "to_barrier": rel[:, 20] - np.nanmax(dfr, 1),
+            "fold": np.nanmax(rel[:, 22:30] - dfr, 1),
+            "barrier1_wait": rel[:, 30] - np.nanmax(rel[:, 22:30], 1),
+            "partition_flush": rel[:, 20] - rel[:, 30],
             "flush": rel[:, 21] - rel[:, 20],
             "end": rel[:, 21],
         }

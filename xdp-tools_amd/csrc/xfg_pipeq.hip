@@ -339,7 +339,8 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	const int tid = threadIdx.x, lane = tid & 63;
 	// (diagnostics: phase stamps, 32 a workgroup -- 0 entry, 1 set-up done,
 	// 2 + w wave w's loop done (10: the count wave's), 11 + w its deferred
-	// walk done, 20 the partitions moved, 21 wave 0's end)
+	// walk done, 22 + w wave w at the first end barrier, 30 past it, 20 the
+	// partitions moved, 21 wave 0's end)
 #ifdef XFG_DIAG
 #define QT_STAMP(slot)                                                                        \
 	do {                                                                                  \
@@ -1360,7 +1361,11 @@ __global__ __launch_bounds__(QT_THREADS(W) + (CW ? 64 : 0), QT_MINW(W)) void xfg
 	}
 	if (lane == 0 && !cwv)
 		s_tn[wv] = tn;
+	if (!cwv)
+		QT_STAMP(22 + wv);
 	__syncthreads();
+	if (tid == 0)
+		QT_STAMP(30);
 	// (every wave's appends are done: done == head) the rest of this
 	// wave's partitions, and the slices' fills for the count kernel; a
 	// position past a slice goes to the counter cache, flushed below
